@@ -1,0 +1,301 @@
+// qlzx_api.hip -- host runtime + C ABI of libqlzx.so (declared in include/qlzx.h).
+//
+// Unity build: the kernel sources are included here so the device tables
+// (qlzx_tables.hip) link without relocatable device code.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "qlzx_tables.hip"
+#include "qlzx_decode_lane.hip"
+#include "qlzx_decode_wave.hip"
+#include "qlzx_encode_lane.hip"
+#include "qlzx_encode_wg.hip"
+#include "qlzx_crc.hip"
+
+namespace {
+
+thread_local std::string t_last_error;
+
+int fail(int code, const char *what, hipError_t e = hipSuccess) {
+    t_last_error = what;
+    if (e != hipSuccess) {
+        t_last_error += ": ";
+        t_last_error += hipGetErrorString(e);
+    }
+    return code;
+}
+
+#define HIP_OK(expr)                                                     \
+    do {                                                                 \
+        hipError_t _e = (expr);                                          \
+        if (_e != hipSuccess) return fail(QLZX_R_HIP, #expr, _e);       \
+    } while (0)
+
+inline uint32_t ld32h(const unsigned char *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+constexpr uint32_t kMaxLaneSlabs = 4096;  // concurrent lane encoders for the general path
+
+}  // namespace
+
+extern "C" {
+
+const char *qlzx_last_error(void) { return t_last_error.c_str(); }
+
+int qlzx_info(char *buf, size_t len) {
+    const char *s =
+        "libqlzx: QuickLZ 1.4.1 level 3 + record CRC32 for gobeansdb; target gfx950 (MI355X); "
+        "decode: wave-per-block LDS history (dsize<=" QLZX_STR(QLZX_FAST_MAX_DSIZE)
+        ") + lane-per-block general; encode: workgroup-per-block position-parallel "
+        "(len<=" QLZX_STR(QLZX_WG_MAX_LEN) ") + lane-per-block general";
+    if (!buf || !len) return (int)strlen(s);
+    snprintf(buf, len, "%s", s);
+    return 0;
+}
+
+/* ---------------- quicklz.h drop-in: header helpers (quicklz.c:674-690) ---------------- */
+size_t qlz_size_decompressed(const char *source) {
+    const unsigned char *s = (const unsigned char *)source;
+    return (s[0] & 2) ? ld32h(s + 5) : s[2];
+}
+size_t qlz_size_compressed(const char *source) {
+    const unsigned char *s = (const unsigned char *)source;
+    return (s[0] & 2) ? ld32h(s + 1) : s[1];
+}
+int qlz_get_setting(int setting) {  // quicklz.c:31-58 as built by quicklz.h:25-31
+    switch (setting) {
+        case 0: return 3;       // QLZ_COMPRESSION_LEVEL
+        case 1: return 528400;  // QLZ_SCRATCH_COMPRESS
+        case 2: return 16;      // QLZ_SCRATCH_DECOMPRESS
+        case 3: return 0;       // QLZ_STREAMING_BUFFER
+        case 6: return 0;       // QLZ_MEMORY_SAFE (the reference build); this library always checks
+        case 7: return 1;
+        case 8: return 4;
+        case 9: return 1;
+    }
+    return -1;
+}
+
+/* ---------------- batch device API ---------------- */
+
+size_t qlzx_decompress_workspace_size(uint32_t n) { return qlzx::decode_wave_ws_bytes(n); }
+
+int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_t *dsize,
+                          int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
+                          uint32_t *crc_out, uint32_t max_dsize, void *workspace,
+                          size_t workspace_bytes, void *stream) {
+    if (!b || !status) return fail(QLZX_R_BAD_ARG, "qlzx_decompress_batch: null blocks/status");
+    if (b->n == 0) return QLZX_R_OK;
+    if (!b->src || !b->src_off || !b->src_len || !b->dst || !b->dst_off)
+        return fail(QLZX_R_BAD_ARG, "qlzx_decompress_batch: null block array");
+    hipStream_t s = (hipStream_t)stream;
+    const bool fast = qlzx::decode_wave_enabled() && workspace_bytes >= qlzx::decode_wave_ws_bytes(b->n) && workspace;
+    if (fast) {
+        int r = qlzx::launch_decode_wave(*b, dst_cap, dsize, status, crc_state, crc_expect, crc_out,
+                                         workspace, s);
+        if (r) return fail(QLZX_R_HIP, "decode_wave launch", (hipError_t)r);
+    }
+    if (!fast || max_dsize > QLZX_FAST_MAX_DSIZE) {
+        const uint32_t min_dsize = fast ? QLZX_FAST_MAX_DSIZE + 1 : 0;
+        hipLaunchKernelGGL(qlzx::k_decode_lane, dim3((b->n + 255) / 256), dim3(256), 0, s, *b, dst_cap,
+                           dsize, status, crc_state, crc_expect, crc_out, min_dsize);
+        HIP_OK(hipGetLastError());
+    }
+    return QLZX_R_OK;
+}
+
+size_t qlzx_compress_workspace_size(uint32_t n, uint32_t max_len) {
+    size_t ws = 0;
+    if (max_len > QLZX_WG_MAX_LEN || !qlzx::encode_wg_enabled())
+        ws = (size_t)std::min<uint32_t>(std::max<uint32_t>(n, 1), kMaxLaneSlabs) * qlzx::kLaneSlab;
+    return std::max(ws, qlzx::encode_wg_ws_bytes(n, max_len));
+}
+
+int qlzx_compress_batch(const qlzx_blocks *b, uint32_t *csize, int32_t *status,
+                        const uint32_t *crc_state, uint32_t *crc_out, uint32_t max_len,
+                        uint32_t flags, void *workspace, size_t workspace_bytes, void *stream) {
+    if (!b || !csize) return fail(QLZX_R_BAD_ARG, "qlzx_compress_batch: null blocks/csize");
+    if (b->n == 0) return QLZX_R_OK;
+    if (!b->src || !b->src_off || !b->src_len || !b->dst || !b->dst_off)
+        return fail(QLZX_R_BAD_ARG, "qlzx_compress_batch: null block array");
+    if (workspace_bytes < qlzx_compress_workspace_size(b->n, max_len) || !workspace)
+        return fail(QLZX_R_WORKSPACE, "qlzx_compress_batch: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    const bool wg = qlzx::encode_wg_enabled() && !(flags & QLZX_F_GO_COMPAT);
+    if (wg) {
+        int r = qlzx::launch_encode_wg(*b, csize, status, crc_state, crc_out, max_len, flags, workspace, s);
+        if (r) return fail(QLZX_R_HIP, "encode_wg launch", (hipError_t)r);
+    }
+    if (!wg || max_len > QLZX_WG_MAX_LEN) {
+        const uint32_t nl = (uint32_t)std::min<size_t>(
+            std::min<uint32_t>(b->n, kMaxLaneSlabs), workspace_bytes / qlzx::kLaneSlab);
+        if (nl == 0) return fail(QLZX_R_WORKSPACE, "qlzx_compress_batch: no lane slab");
+        const uint32_t min_len = wg ? QLZX_WG_MAX_LEN + 1 : 0;
+        hipLaunchKernelGGL(qlzx::k_encode_lane, dim3((nl + 63) / 64), dim3(64), 0, s, *b, csize, status,
+                           crc_state, crc_out, (uint8_t *)workspace, nl, min_len, flags);
+        HIP_OK(hipGetLastError());
+    }
+    return QLZX_R_OK;
+}
+
+int qlzx_crc32_batch(const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len, uint32_t n,
+                     const uint32_t *init, uint32_t final_xor, uint32_t *out, void *stream) {
+    if (n == 0) return QLZX_R_OK;
+    if (!src || !src_off || !src_len || !out) return fail(QLZX_R_BAD_ARG, "qlzx_crc32_batch: null arg");
+    hipLaunchKernelGGL(qlzx::k_crc32, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, src, src_off,
+                       src_len, n, init, final_xor, out);
+    HIP_OK(hipGetLastError());
+    return QLZX_R_OK;
+}
+
+int qlzx_synth_batch(int kind, uint64_t seed, uint64_t first_id, uint8_t *dst, const uint64_t *dst_off,
+                     const uint32_t *len, uint32_t n, const uint8_t *vocab, const uint32_t *vocab_off,
+                     const uint32_t *zipf_cdf, uint32_t nwords, void *stream) {
+    if (n == 0) return QLZX_R_OK;
+    if (!dst || !dst_off || !len || !vocab || !vocab_off || !zipf_cdf || nwords == 0)
+        return fail(QLZX_R_BAD_ARG, "qlzx_synth_batch: null arg");
+    hipLaunchKernelGGL(qlzx::k_synth, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, kind, seed,
+                       first_id, dst, dst_off, len, n, vocab, vocab_off, zipf_cdf, nwords);
+    HIP_OK(hipGetLastError());
+    return QLZX_R_OK;
+}
+
+}  // extern "C"
+
+/* ---------------- single-call runtime (quicklz.h drop-in on the GPU) ----------------
+ * Each calling thread owns a stream and device/pinned staging buffers, so the
+ * symbols are re-entrant like the reference (quicklz.h: one scratch per call). */
+namespace {
+
+struct Ctx {
+    hipStream_t s = nullptr;
+    uint8_t *d_buf = nullptr;  // [src | dst | meta | ws]
+    size_t d_cap = 0;
+    uint8_t *h_meta = nullptr;  // pinned 4 KiB
+    bool ok = false;
+    ~Ctx() {
+        if (d_buf) (void)hipFree(d_buf);
+        if (h_meta) (void)hipHostFree(h_meta);
+        if (s) (void)hipStreamDestroy(s);
+    }
+    int init() {
+        if (ok) return 0;
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(QLZX_R_NO_DEVICE, "no HIP device");
+        HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        HIP_OK(hipHostMalloc((void **)&h_meta, 4096, hipHostMallocDefault));
+        ok = true;
+        return 0;
+    }
+    int reserve(size_t bytes) {
+        if (bytes <= d_cap) return 0;
+        if (d_buf) (void)hipFree(d_buf);
+        d_buf = nullptr;
+        d_cap = 0;
+        const size_t want = align_up(bytes + bytes / 4, 1 << 20);
+        HIP_OK(hipMalloc((void **)&d_buf, want));
+        d_cap = want;
+        return 0;
+    }
+};
+thread_local Ctx t_ctx;
+
+struct Meta {  // one-block batch descriptors, device side
+    uint64_t src_off, dst_off;
+    uint32_t src_len, dst_cap, out_size, crc_in, crc_out;
+    int32_t status;
+};
+
+}  // namespace
+
+extern "C" {
+
+size_t qlz_compress(const void *source, char *destination, size_t size, char *scratch_compress) {
+    (void)scratch_compress;
+    return qlzx_compress1(source, destination, size, 0);
+}
+
+size_t qlzx_compress1(const void *source, char *destination, size_t size, uint32_t flags) {
+    if (size == 0 || size > 0xffffffffull - 400) return 0;  // quicklz.c:705-706
+    Ctx &c = t_ctx;
+    if (c.init()) return 0;
+    const size_t src_b = align_up(size, 256), dst_b = align_up(size + 400, 256);
+    const size_t ws_b = qlzx_compress_workspace_size(1, (uint32_t)size);
+    if (c.reserve(src_b + dst_b + 256 + ws_b)) return 0;
+    uint8_t *d_src = c.d_buf, *d_dst = d_src + src_b, *d_meta = d_dst + dst_b, *d_ws = d_meta + 256;
+    Meta *m = (Meta *)c.h_meta;
+    memset(m, 0, sizeof(Meta));
+    m->src_len = (uint32_t)size;
+    if (hipMemcpyAsync(d_src, source, size, hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
+    if (hipMemcpyAsync(d_meta, m, sizeof(Meta), hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
+    Meta *dm = (Meta *)d_meta;
+    qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
+    if (qlzx_compress_batch(&b, &dm->out_size, &dm->status, nullptr, nullptr, (uint32_t)size, flags, d_ws,
+                            ws_b, c.s))
+        return 0;
+    if (hipMemcpyAsync(m, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
+    if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
+    if (m->status != QLZX_OK || m->out_size == 0) return 0;
+    if (hipMemcpyAsync(destination, d_dst, m->out_size, hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
+    if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
+    return m->out_size;
+}
+
+size_t qlz_decompress(const char *source, void *destination, char *scratch_decompress) {
+    (void)scratch_decompress;
+    const size_t csize = qlz_size_compressed(source), dsize = qlz_size_decompressed(source);
+    if (csize < 3) return 0;
+    Ctx &c = t_ctx;
+    if (c.init()) return 0;
+    const size_t src_b = align_up(csize, 256), dst_b = align_up(dsize + 1, 256);
+    const size_t ws_b = align_up(qlzx_decompress_workspace_size(1), 256);
+    if (c.reserve(src_b + dst_b + 256 + ws_b)) return 0;
+    uint8_t *d_src = c.d_buf, *d_dst = d_src + src_b, *d_meta = d_dst + dst_b, *d_ws = d_meta + 256;
+    Meta *m = (Meta *)c.h_meta;
+    memset(m, 0, sizeof(Meta));
+    m->src_len = (uint32_t)csize;
+    m->dst_cap = (uint32_t)dsize;
+    if (hipMemcpyAsync(d_src, source, csize, hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
+    if (hipMemcpyAsync(d_meta, m, sizeof(Meta), hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
+    Meta *dm = (Meta *)d_meta;
+    qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
+    if (qlzx_decompress_batch(&b, &dm->dst_cap, &dm->out_size, &dm->status, nullptr, nullptr, nullptr,
+                              (uint32_t)dsize, d_ws, ws_b, c.s))
+        return 0;
+    if (hipMemcpyAsync(m, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
+    if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
+    if (m->status != QLZX_OK) return 0;
+    if (dsize && hipMemcpyAsync(destination, d_dst, dsize, hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
+    if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
+    return m->out_size;
+}
+
+uint32_t crc32_write(uint32_t crc, unsigned char *buf, int len) {
+    if (len <= 0) return crc;  // store/crc32.go:65 loops zero times
+    Ctx &c = t_ctx;
+    if (c.init()) return crc;
+    const size_t src_b = align_up((size_t)len, 256);
+    if (c.reserve(src_b + 256)) return crc;
+    uint8_t *d_src = c.d_buf, *d_meta = d_src + src_b;
+    Meta *m = (Meta *)c.h_meta;
+    memset(m, 0, sizeof(Meta));
+    m->src_len = (uint32_t)len;
+    m->crc_in = crc;
+    if (hipMemcpyAsync(d_src, buf, len, hipMemcpyHostToDevice, c.s) != hipSuccess) return crc;
+    if (hipMemcpyAsync(d_meta, m, sizeof(Meta), hipMemcpyHostToDevice, c.s) != hipSuccess) return crc;
+    Meta *dm = (Meta *)d_meta;
+    if (qlzx_crc32_batch(d_src, &dm->src_off, &dm->src_len, 1, &dm->crc_in, 0, &dm->crc_out, c.s)) return crc;
+    if (hipMemcpyAsync(m, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return crc;
+    if (hipStreamSynchronize(c.s) != hipSuccess) return crc;
+    return m->crc_out;
+}
+
+}  // extern "C"

@@ -1,0 +1,112 @@
+// qlzx_device.h -- device-side helpers shared by the gfx950 kernels.
+//
+// QuickLZ level-3 format facts used here (SURVEY.md §8 "Format facts"):
+//   header byte 0 = 01SSLLHC (quicklz.c:771-772); 9-byte header if H
+//   control word: 32-bit LE, LSB-first item bits, bit 31 sentinel (quicklz.c:203,221)
+//   level-3 match tokens (quicklz.c:579-610)
+//   last 10 output bytes are always literals (quicklz.c:204, 503)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/qlzx.h"
+
+#define QLZX_TAIL 10u         // UNCONDITIONAL_MATCHLEN + UNCOMPRESSED_END (quicklz.c:24-25)
+#define QLZX_BUCKETS 4096u    // QLZ_HASH_VALUES (quicklz.h:62)
+#define QLZX_SLOTS 16u        // QLZ_POINTERS    (quicklz.h:61)
+#define QLZX_MAX_OFFSET 131071u
+#define QLZX_STR_(x) #x
+#define QLZX_STR(x) QLZX_STR_(x)
+
+namespace qlzx {
+
+// CRC-32/IEEE reflected table, poly 0xEDB88320 (store/crc32.go:5-59).
+extern __device__ uint32_t g_crc_table[256];
+// g_crc_x8n[k] = x^(8 * 2^k) mod P in reflected form, for CRC shift/combine.
+extern __device__ uint32_t g_crc_pow[64];
+
+constexpr uint32_t CRC_POLY = 0xEDB88320u;
+
+// GF(2) product a*b mod P, reflected representation (bit 31 = x^0).
+__device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll 8
+    for (int i = 0; i < 32; i++) {
+        p ^= (a & 0x80000000u) ? b : 0u;
+        a <<= 1;
+        b = (b & 1u) ? (b >> 1) ^ CRC_POLY : (b >> 1);
+    }
+    return p;
+}
+
+// Raw CRC state advanced over `nbytes` zero bytes: s * x^(8n) mod P.
+__device__ __forceinline__ uint32_t crc_shift(uint32_t s, uint64_t nbytes) {
+    uint32_t k = 0;
+    while (nbytes) {
+        if (nbytes & 1u) s = gf2_mulmod(g_crc_pow[k], s);
+        nbytes >>= 1;
+        k++;
+    }
+    return s;
+}
+
+__device__ __forceinline__ uint32_t crc_byte(const uint32_t *tab, uint32_t c, uint32_t b) {
+    return tab[(c ^ b) & 0xffu] ^ (c >> 8);
+}
+
+__device__ __forceinline__ uint32_t crc_word(const uint32_t *tab, uint32_t c, uint32_t w) {
+    c = crc_byte(tab, c, w & 0xff);
+    c = crc_byte(tab, c, (w >> 8) & 0xff);
+    c = crc_byte(tab, c, (w >> 16) & 0xff);
+    return crc_byte(tab, c, w >> 24);
+}
+
+// Load the CRC table into LDS (call by the whole block, then __syncthreads()).
+__device__ __forceinline__ void load_crc_table(uint32_t *lds_tab) {
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) lds_tab[i] = g_crc_table[i];
+}
+
+__device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
+__device__ __forceinline__ uint32_t ld_u32_bytes(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// Level-3 token decode (quicklz.c:579-610): returns token length in bytes.
+__device__ __forceinline__ uint32_t decode_token(uint32_t t, uint32_t &off, uint32_t &len) {
+    if ((t & 3u) == 0) { off = (t & 0xffu) >> 2; len = 3; return 1; }
+    if ((t & 2u) == 0) { off = (t & 0xffffu) >> 2; len = 3; return 2; }
+    if ((t & 1u) == 0) { off = (t & 0xffffu) >> 6; len = ((t >> 2) & 15u) + 3; return 2; }
+    if ((t & 127u) != 3) { off = (t >> 7) & 0x1ffffu; len = ((t >> 2) & 0x1fu) + 2; return 3; }
+    off = t >> 15; len = ((t >> 7) & 255u) + 3; return 4;
+}
+
+// Token length from its first byte alone.
+__device__ __forceinline__ uint32_t token_bytes(uint32_t b0) {
+    if ((b0 & 3u) == 0) return 1;
+    if ((b0 & 3u) != 3) return 2;
+    return ((b0 & 127u) != 3) ? 3 : 4;
+}
+
+struct Header {
+    uint32_t hdr, csize, dsize;
+    bool compressed;
+    uint32_t level;
+};
+
+__device__ __forceinline__ Header parse_header(const uint8_t *s) {
+    Header h;
+    const uint32_t b0 = s[0];
+    h.hdr = (b0 & 2u) ? 9u : 3u;
+    h.compressed = (b0 & 1u) != 0;
+    h.level = (b0 >> 2) & 3u;
+    if (h.hdr == 9) {
+        h.csize = ld_u32_bytes(s + 1);
+        h.dsize = ld_u32_bytes(s + 5);
+    } else {
+        h.csize = s[1];
+        h.dsize = s[2];
+    }
+    return h;
+}
+
+}  // namespace qlzx

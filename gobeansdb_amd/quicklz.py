@@ -1,0 +1,151 @@
+"""Mirror of gobeansdb's ``quicklz`` Go package (quicklz/quicklz.go, quicklz/cquicklz.go).
+
+Same names, argument meaning and error behaviour, so the parity tests read
+like ``quicklz/quicklz_test.go``.  Go's ``(value, error)`` pairs are returned
+as tuples; Go panics are raised.  Every codec call runs on the GPU through
+libqlzx.so (include/qlzx.h); there is no CPU codec here.
+
+    Go                                   here
+    SizeCompressed(src) int              SizeCompressed(src) -> int      quicklz.go:46
+    SizeDecompressed(src) int            SizeDecompressed(src) -> int    quicklz.go:39
+    CCompress(src) (CArray, bool)        CCompress(src) -> (CArray, bool) cquicklz.go:23
+    CDecompress(src, sizeD) (CArray, err) CDecompress(src, n) -> (CArray, err) cquicklz.go:44
+    CDecompressSafe(src) (CArray, err)   CDecompressSafe(src)            cquicklz.go:84
+    DecompressSafe(src) ([]byte, err)    DecompressSafe(src)             cquicklz.go:62
+    Compress(src, level) []byte          Compress(src, level)            quicklz.go:80
+    Decompress(src) []byte               Decompress(src)                 quicklz.go:291
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib
+
+CompressBufferSize = 528400   # cquicklz.go:19
+DecompressBufferSize = 16     # cquicklz.go:20
+BodyInC = 4096                # config/mc_config.go:9 (cmem.CArray: Go heap below, C heap above)
+
+
+class QuicklzError(Exception):
+    pass
+
+
+class CArray:
+    """cmem.CArray (cmem/cmem.go): Body plus the allocation size Cap."""
+
+    __slots__ = ("Body", "Cap")
+
+    def __init__(self, body: bytes = b"", cap: int = 0):
+        self.Body = body
+        self.Cap = cap
+
+    def Free(self) -> None:  # cmem.go:96-104
+        self.Body = b""
+        self.Cap = 0
+
+
+def _as_bytes(src) -> bytes:
+    return bytes(src)
+
+
+def SizeDecompressed(source) -> int:
+    """quicklz.go:39-44 (header parse; reads byte 0 and the size field)."""
+    s = _as_bytes(source)
+    if s[0] & 2:
+        return int.from_bytes(s[5:9], "little")
+    return s[2]
+
+
+def SizeCompressed(source) -> int:
+    """quicklz.go:46-51."""
+    s = _as_bytes(source)
+    if s[0] & 2:
+        return int.from_bytes(s[1:5], "little")
+    return s[1]
+
+
+def CCompress(src) -> tuple[CArray, bool]:
+    """cquicklz.go:23-42: C-library level-3 compress into a len+400 CArray.
+
+    ``&src[0]`` panics on an empty slice (cquicklz.go:36): IndexError here."""
+    s = _as_bytes(src)
+    if len(s) == 0:
+        raise IndexError("index out of range [0] with length 0")
+    dst = ctypes.create_string_buffer(len(s) + 400)
+    n = _lib.lib().qlz_compress(s, dst, len(s), None)
+    if n == 0:
+        raise _lib.QlzxError("qlz_compress failed: " + _lib.lib().qlzx_last_error().decode())
+    return CArray(dst.raw[:n], len(s) + 400), True
+
+
+def CDecompress(src, sizeD: int) -> tuple[CArray, QuicklzError | None]:
+    """cquicklz.go:44-60."""
+    s = _as_bytes(src)
+    dst = ctypes.create_string_buffer(max(sizeD, 1))
+    size = _lib.lib().qlz_decompress(s, dst, None)
+    if size != sizeD:
+        return CArray(), QuicklzError(f"fail to alloc for decompress, size {sizeD} != {size}")
+    return CArray(dst.raw[:size], sizeD), None
+
+
+def CDecompressSafe(src) -> tuple[CArray, QuicklzError | None]:
+    """cquicklz.go:84-101: size-checked CDecompress."""
+    s = _as_bytes(src)
+    try:
+        sizeC = SizeCompressed(s)
+    except IndexError as e:  # recover() in the Go wrapper
+        return CArray(), QuicklzError(f"CDecompressSafe panic({e!r})")
+    if len(s) != sizeC:
+        return CArray(), QuicklzError(f"bad sizeCompressed, expect {sizeC}, got {len(s)}")
+    return CDecompress(s, SizeDecompressed(s))
+
+
+def Compress(source, level: int) -> bytes | None:
+    """quicklz.go:80-289: Go encoder.  Level 3 differs from CCompress in three
+    ways (always a 9-byte header, earlier bail-out, nil on empty), reproduced
+    by the GPU encoder's GO_COMPAT mode.  Level 1 is not built."""
+    if level not in (1, 3):
+        raise QuicklzError("Go version only supports level 1 and 3")   # quicklz.go:94-96
+    if level == 1:
+        raise NotImplementedError("QuickLZ level-1 encoding is outside this build (DESIGN.md §7)")
+    s = _as_bytes(source)
+    if len(s) == 0:
+        return None   # quicklz.go:109-111
+    dst = ctypes.create_string_buffer(len(s) + 400)
+    n = _lib.lib().qlzx_compress1(s, dst, len(s), _lib.F_GO_COMPAT)
+    if n == 0:
+        raise _lib.QlzxError("qlzx_compress1 failed: " + _lib.lib().qlzx_last_error().decode())
+    return dst.raw[:n]
+
+
+def Decompress(source) -> bytes:
+    """quicklz.go:291-431.  Level 3 streams (level 1 raises, as Go panics for
+    levels other than 1/3 and this build decodes level 3 only)."""
+    s = _as_bytes(source)
+    level = (s[0] >> 2) & 3
+    if level not in (1, 3):
+        raise QuicklzError("Go version only supports level 1 and 3")
+    if level == 1:
+        raise NotImplementedError("QuickLZ level-1 decoding is outside this build (DESIGN.md §7)")
+    n = SizeDecompressed(s)
+    dst = ctypes.create_string_buffer(max(n, 1))
+    size = _lib.lib().qlz_decompress(s, dst, None)
+    if size != n:
+        raise QuicklzError(f"corrupt quicklz stream (status {_lib.lib().qlzx_last_error().decode()})")
+    return dst.raw[:n]
+
+
+def DecompressSafe(src) -> tuple[bytes | None, QuicklzError | None]:
+    """cquicklz.go:62-82."""
+    s = _as_bytes(src)
+    try:
+        sizeC = SizeCompressed(s)
+        if len(s) != sizeC:
+            return None, QuicklzError(f"bad sizeCompressed, expect {sizeC}, got {len(s)}")
+        sizeD = SizeDecompressed(s)
+        dst = Decompress(s)
+    except (QuicklzError, IndexError) as e:
+        return None, QuicklzError(f"decompress panic with non-error: {e!r}")
+    if len(dst) != sizeD:
+        return None, QuicklzError(f"bad sizeDecompressed, expect {sizeD}, got {len(dst)}")
+    return dst, None

@@ -1,0 +1,183 @@
+"""GPU parity: the HIP codec through the C ABI vs the reference golden vectors and the oracle."""
+import ctypes
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+KAT = (b"LZ compression is based on finding repeated strings: Five, six, seven, eight, nine, "
+       b"fifteen, sixteen, seventeen, fifteen, sixteen, seventeen.")
+
+
+def _gpu_compress(blocks, **kw):
+    import torch
+    from gobeansdb_amd import batch
+    src = batch.BlockBatch.from_bytes(blocks)
+    dst, csize, status, crc = batch.compress(src, **kw)
+    torch.cuda.synchronize()
+    cs = csize.cpu().numpy().view(np.uint32)
+    return dst.to_bytes(cs), status.cpu().numpy(), (None if crc is None else crc.cpu().numpy().view(np.uint32))
+
+
+def _gpu_decompress(comp, caps=None, **kw):
+    import torch
+    from gobeansdb_amd import batch
+    src = batch.BlockBatch.from_bytes(comp)
+    sizes = [O.lib().orc_size_decompressed(np.frombuffer(c + bytes(9), np.uint8).ctypes.data) if len(c) >= 3 else 0
+             for c in comp]
+    caps_arr = sizes if caps is None else caps
+    out = batch.BlockBatch.empty_for([max(s, 1) for s in caps_arr])
+    cap_t = torch.tensor(np.asarray(caps_arr, dtype=np.uint32).view(np.int32), device="cuda")
+    dsize, status, crc = batch.decompress(src, out, dst_cap=cap_t, max_dsize=max(caps_arr + [1]), **kw)
+    torch.cuda.synchronize()
+    ds = dsize.cpu().numpy().view(np.uint32)
+    return out.to_bytes(ds), status.cpu().numpy(), (None if crc is None else crc.cpu().numpy().view(np.uint32))
+
+
+def test_compress_golden_bit_exact(cuda, golden):
+    vs = golden.vectors
+    outs, st, crc = _gpu_compress([golden.get(v["input"]) for v in vs], want_crc=True)
+    assert (st == 0).all()
+    for v, o, c in zip(vs, outs, crc):
+        assert o == golden.get(v["c_out"]), v["name"]
+        assert int(c) == v["crc_c_out"], v["name"]   # fused CRC over the compressed value
+
+
+def test_decompress_golden(cuda, golden):
+    vs = golden.vectors
+    outs, st, crc = _gpu_decompress([golden.get(v["c_out"]) for v in vs], want_crc=True)
+    assert (st == 0).all(), [(v["name"], s) for v, s in zip(vs, st) if s]
+    for v, o, c in zip(vs, outs, crc):
+        assert o == golden.get(v["input"]), v["name"]
+        assert int(c) == v["crc_c_out"]
+
+
+def test_quicklz_go_api_kat(cuda):
+    """quicklz/quicklz_test.go:7-34, against the GPU-backed mirror."""
+    from gobeansdb_amd.quicklz import (CCompress, CDecompress, Compress, Decompress,
+                                       SizeCompressed, SizeDecompressed)
+    orig = KAT
+    compressed = Compress(orig, 3)
+    l, lc = len(orig), len(compressed)
+    assert lc == 116
+    s, sc = SizeDecompressed(compressed), SizeCompressed(compressed)
+    assert s == l and sc == lc
+    assert len(Decompress(compressed)) == l
+    compressed2, ok = CCompress(orig)
+    assert ok
+    decompressed2, err = CDecompress(compressed2.Body, s)
+    assert err is None and decompressed2.Body == orig
+
+
+def test_single_call_symbols(cuda, golden):
+    from gobeansdb_amd import _lib
+    L = _lib.lib()
+    for v in golden.vectors[::7]:
+        data, c = golden.get(v["input"]), golden.get(v["c_out"])
+        dst = ctypes.create_string_buffer(len(data) + 400)
+        n = L.qlz_compress(data, dst, len(data), ctypes.create_string_buffer(528400))
+        assert dst.raw[:n] == c, v["name"]
+        out = ctypes.create_string_buffer(len(data) + 1)
+        assert L.qlz_decompress(c, out, ctypes.create_string_buffer(16)) == len(data)
+        assert out.raw[:len(data)] == data
+        assert L.crc32_write(0xFFFFFFFF, data, len(data)) ^ 0xFFFFFFFF == v["crc_in"]
+    assert L.qlz_compress(b"", ctypes.create_string_buffer(400), 0, None) == 0   # quicklz.c:705
+
+
+def test_cdecompress_safe_errors(cuda, golden):
+    from gobeansdb_amd.quicklz import CDecompressSafe
+    c = golden.get([v for v in golden.vectors if v["name"] == "text_4096"][0]["c_out"])
+    arr, err = CDecompressSafe(c[:-1])
+    assert err is not None and "bad sizeCompressed" in str(err)
+    arr, err = CDecompressSafe(c)
+    assert err is None and len(arr.Body) == 4096
+
+
+def test_corrupt_status_matches_oracle(cuda, golden):
+    rng = np.random.default_rng(5)
+    base = [golden.get(v["c_out"]) for v in golden.vectors if v["cls"] in ("text", "runs", "kat") and v["n"] >= 100]
+    cases = []
+    for c in base:
+        for _ in range(6):
+            b = bytearray(c)
+            hdr = 9 if b[0] & 2 else 3
+            k = int(rng.integers(hdr, len(b)))
+            b[k] = int(rng.integers(0, 256))
+            cases.append(bytes(b))
+        cases.append(c[:-1])
+    caps = [O.lib().orc_size_decompressed(np.frombuffer(c + bytes(9), np.uint8).ctypes.data) for c in cases]
+    caps = [min(x, 1 << 20) for x in caps]
+    outs, st, _ = _gpu_decompress(cases, caps=caps)
+    for c, cap, o, s in zip(cases, caps, outs, st):
+        ost, od = O.decompress(c, cap=cap)
+        assert s == ost
+        if s == 0:
+            assert o == od
+
+
+def test_crc_batch(cuda, golden):
+    import torch
+    from gobeansdb_amd import batch
+    datas = [golden.get(v["input"]) for v in golden.vectors]
+    src = batch.BlockBatch.from_bytes(datas)
+    out = batch.crc32(src).cpu().numpy().view(np.uint32)
+    for d, v, c in zip(datas, golden.vectors, out):
+        assert int(c) == (zlib.crc32(d) if d else 0), v["name"]
+    init = torch.tensor(np.full(len(datas), 0x12345678, np.uint32).view(np.int32), device="cuda")
+    raw = batch.crc32(src, init=init, final_xor=0).cpu().numpy().view(np.uint32)
+    for d, c in zip(datas, raw):
+        assert int(c) == O.crc32_write(0x12345678, d)
+
+
+@pytest.mark.parametrize("kind", ["text", "image"])
+def test_synth_matches_oracle(cuda, kind):
+    import torch
+    from gobeansdb_amd import batch
+    lens = [16384, 65536, 5, 4096, 777]
+    b = batch.synth(kind, 1234, lens, first_id=100)
+    torch.cuda.synchronize()
+    got = b.to_bytes()
+    gen = O.gen_text if kind == "text" else O.gen_image
+    for i, n in enumerate(lens):
+        assert got[i] == gen(1234, 100 + i, n)
+
+
+def test_go_compat_compress(cuda):
+    blocks = [O.gen_text(99, n, n) for n in (1, 4, 5, 215, 216, 4096)] + [O.gen_image(3, 0, 4096), KAT]
+    outs, st, _ = _gpu_compress(blocks, go_compat=True)
+    assert (st == 0).all()
+    for b, o in zip(blocks, outs):
+        assert o == O.compress_go(b)
+
+
+def test_record_fused_crc_verify(cuda, golden):
+    """store/datafile.go:161-168: CRC over header[4:24] ‖ key ‖ value, fused with decompress."""
+    import struct
+    import torch
+    data = golden.records_data
+    comp, states, expect, values = [], [], [], []
+    for r in golden.records:
+        if not r["flag"] & 0x10000:
+            continue
+        o = r["offset"]
+        crc, ts, flag, ver, ksz, vsz = struct.unpack_from("<IIIiII", data, o)
+        key = data[o + 24:o + 24 + ksz]
+        body = data[o + 24 + ksz:o + 24 + ksz + vsz]
+        st = O.crc32_write(O.crc32_write(0xFFFFFFFF, data[o + 4:o + 24]), key)
+        comp.append(body), states.append(st), expect.append(crc), values.append(golden.get(r["value"]))
+    # flip one byte of one record's value to force a CRC failure
+    bad = bytearray(comp[1])
+    bad[len(bad) // 2] ^= 0x40
+    comp[1] = bytes(bad)
+    s_t = torch.tensor(np.asarray(states, np.uint32).view(np.int32), device="cuda")
+    e_t = torch.tensor(np.asarray(expect, np.uint32).view(np.int32), device="cuda")
+    outs, st, crc = _gpu_decompress(comp, crc_state=s_t, crc_expect=e_t)
+    for i, (o, s, v) in enumerate(zip(outs, st, values)):
+        if i == 1:
+            assert s == 5   # QLZX_E_CRC
+        else:
+            assert s == 0 and o == v

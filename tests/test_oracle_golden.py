@@ -1,0 +1,102 @@
+"""The CPU oracle against the reference's golden vectors (no GPU).
+
+Pins oracle/qlz_oracle.c to quicklz/quicklz.c + store/crc32.go output captured
+by tests/golden/make_golden.py, and to quicklz/quicklz_test.go's KAT."""
+import struct
+import zlib
+
+import pytest
+
+from oracle import oracle as O
+
+KAT = (b"LZ compression is based on finding repeated strings: Five, six, seven, eight, nine, "
+       b"fifteen, sixteen, seventeen, fifteen, sixteen, seventeen.")
+
+
+def test_kat_go_and_c_lengths():
+    # quicklz_test.go:10-14: Go Compress(orig, 3) is 116 B; the C library writes a 3-byte header
+    assert len(O.compress_go(KAT)) == 116
+    assert len(O.compress(KAT)) == 110
+    assert O.compress_go(KAT)[9:] == O.compress(KAT)[3:]   # same core stream
+    st, d = O.decompress(O.compress_go(KAT))
+    assert st == O.OK and d == KAT
+
+
+def test_vectors_compress_bit_exact(golden):
+    for v in golden.vectors:
+        data = golden.get(v["input"])
+        assert O.compress(data) == golden.get(v["c_out"]), v["name"]
+
+
+def test_vectors_roundtrip_and_crc(golden):
+    for v in golden.vectors:
+        data, c = golden.get(v["input"]), golden.get(v["c_out"])
+        st, d = O.decompress(c)
+        assert st == O.OK and d == data, v["name"]
+        assert (O.crc32_write(0xFFFFFFFF, data) ^ 0xFFFFFFFF) == v["crc_in"] == zlib.crc32(data)
+        assert (O.crc32_write(0xFFFFFFFF, c) ^ 0xFFFFFFFF) == v["crc_c_out"]
+
+
+def test_headers(golden):
+    for v in golden.vectors:
+        c = golden.get(v["c_out"])
+        hdr = 9 if c[0] & 2 else 3
+        assert hdr == (3 if v["n"] < 216 else 9)                       # quicklz.c:708-711
+        assert c[0] & 0xFC == 0x4C                                     # 01 SS=00 LL=11
+        csz = int.from_bytes(c[1:5], "little") if hdr == 9 else c[1]
+        dsz = int.from_bytes(c[5:9], "little") if hdr == 9 else c[2]
+        assert csz == len(c) and dsz == v["n"]
+        if not c[0] & 1:
+            assert len(c) == v["n"] + hdr                              # stored block
+
+
+def test_offset_limit_vector(golden):
+    v = [v for v in golden.vectors if v["cls"] == "far"][0]
+    assert golden.get(v["c_out"])[0] & 1
+
+
+def test_corrupt_streams_are_rejected(golden):
+    v = [v for v in golden.vectors if v["name"] == "text_16384"][0]
+    c = bytearray(golden.get(v["c_out"]))
+    assert O.decompress(bytes(c[:-1]))[0] == O.E_SIZE_COMPRESSED
+    bad = bytearray(c)
+    bad[0] = (bad[0] & ~0x0C) | 0x04                                    # level 1
+    assert O.decompress(bytes(bad))[0] == O.E_LEVEL
+    assert O.decompress(bytes(c), cap=100)[0] == O.E_DST_CAP
+    # a token whose offset reaches before the block start
+    z = bytearray(9 + 4 + 4 + 20)
+    z[0] = 0x4F
+    z[1:5] = len(z).to_bytes(4, "little")
+    z[5:9] = (40).to_bytes(4, "little")
+    z[9:13] = (0x80000000 | 1).to_bytes(4, "little")                    # first item = match
+    z[13] = 60 << 2                                                     # 1-byte token, off 60 > op 0
+    assert O.decompress(bytes(z))[0] == O.E_CORRUPT
+
+
+def test_records_fixture(golden):
+    """records.data follows store/datafile.go:66-102 with reference CRCs."""
+    data = golden.records_data
+    for r in golden.records:
+        o = r["offset"]
+        crc, ts, flag, ver, ksz, vsz = struct.unpack_from("<IIIiII", data, o)
+        assert (crc, ts, flag, ver, vsz) == (r["crc"], r["ts"], r["flag"], r["ver"], r["vsz"])
+        key = data[o + 24:o + 24 + ksz]
+        body = data[o + 24 + ksz:o + 24 + ksz + vsz]
+        assert O.record_crc(data[o + 4:o + 24], key, body) == crc
+        value = golden.get(r["value"])
+        if flag & 0x10000:
+            st, d = O.decompress(body)
+            assert st == O.OK and d == value
+        else:
+            assert body == value
+    # store/data_test.go:41-47: "v"*255 fits one 256-B slot, 400 random bytes need two
+    sizes = [((24 + len(r["key"]) + r["vsz"] + 255) // 256) for r in golden.records[:4]]
+    assert sizes == [1, 1, 2, 3]
+
+
+@pytest.mark.parametrize("n", [1, 4, 5, 215, 216, 4096])
+def test_go_compat_mode(n):
+    data = O.gen_text(99, n, n)
+    g = O.compress_go(data)
+    assert g[0] & 2 and int.from_bytes(g[1:5], "little") == len(g)
+    assert O.decompress(g) == (O.OK, data)
