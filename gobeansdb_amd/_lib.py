@@ -66,7 +66,7 @@ def lib() -> ctypes.CDLL:
     L.crc32_write.argtypes = [u32, vp, ctypes.c_int]
     L.crc32_write.restype = u32
     BP = ctypes.POINTER(Blocks)
-    L.qlzx_decompress_workspace_size.argtypes = [u32]
+    L.qlzx_decompress_workspace_size.argtypes = [u32, u32]
     L.qlzx_decompress_workspace_size.restype = sz
     L.qlzx_decompress_batch.argtypes = [BP, vp, vp, vp, vp, vp, vp, u32, vp, sz, vp]
     L.qlzx_decompress_batch.restype = ctypes.c_int

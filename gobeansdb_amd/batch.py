@@ -104,11 +104,11 @@ def decompress(src: BlockBatch, dst: BlockBatch, *, dst_cap: torch.Tensor | None
     dsize = torch.zeros(n, dtype=torch.int32, device=dev)
     status = torch.full((n,), -1, dtype=torch.int32, device=dev)
     crc_out = torch.zeros(n, dtype=torch.int32, device=dev) if (want_crc or crc_expect is not None) else None
-    ws_bytes = L.qlzx_decompress_workspace_size(n)
-    ws = (workspace or Workspace(dev)).get(ws_bytes)
-    b = _blocks(src, dst.data, dst.off)
     if max_dsize is None:
         max_dsize = 0xFFFFFFFF
+    ws_bytes = L.qlzx_decompress_workspace_size(n, max_dsize)
+    ws = (workspace or Workspace(dev)).get(ws_bytes)
+    b = _blocks(src, dst.data, dst.off)
     rc = L.qlzx_decompress_batch(ctypes.byref(b), _ptr(dst_cap), dsize.data_ptr(), status.data_ptr(),
                                  _ptr(crc_state), _ptr(crc_expect), _ptr(crc_out), max_dsize,
                                  ws.data_ptr(), ws_bytes, _stream(stream))

@@ -86,7 +86,9 @@ int qlz_get_setting(int setting) {  // quicklz.c:31-58 as built by quicklz.h:25-
 
 /* ---------------- batch device API ---------------- */
 
-size_t qlzx_decompress_workspace_size(uint32_t n) { return qlzx::decode_wave_ws_bytes(n); }
+size_t qlzx_decompress_workspace_size(uint32_t n, uint32_t max_dsize) {
+    return qlzx::decode_wave_ws_bytes(n, max_dsize);
+}
 
 int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_t *dsize,
                           int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
@@ -97,10 +99,11 @@ int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_
     if (!b->src || !b->src_off || !b->src_len || !b->dst || !b->dst_off)
         return fail(QLZX_R_BAD_ARG, "qlzx_decompress_batch: null block array");
     hipStream_t s = (hipStream_t)stream;
-    const bool fast = qlzx::decode_wave_enabled() && workspace_bytes >= qlzx::decode_wave_ws_bytes(b->n) && workspace;
+    const bool fast = qlzx::decode_wave_enabled() && workspace &&
+                      workspace_bytes >= qlzx::decode_wave_ws_bytes(b->n, max_dsize);
     if (fast) {
         int r = qlzx::launch_decode_wave(*b, dst_cap, dsize, status, crc_state, crc_expect, crc_out,
-                                         workspace, s);
+                                         max_dsize, workspace, workspace_bytes, s);
         if (r) return fail(QLZX_R_HIP, "decode_wave launch", (hipError_t)r);
     }
     if (!fast || max_dsize > QLZX_FAST_MAX_DSIZE) {
@@ -256,7 +259,7 @@ size_t qlz_decompress(const char *source, void *destination, char *scratch_decom
     Ctx &c = t_ctx;
     if (c.init()) return 0;
     const size_t src_b = align_up(csize, 256), dst_b = align_up(dsize + 1, 256);
-    const size_t ws_b = align_up(qlzx_decompress_workspace_size(1), 256);
+    const size_t ws_b = align_up(qlzx_decompress_workspace_size(1, (uint32_t)dsize), 256);
     if (c.reserve(src_b + dst_b + 256 + ws_b)) return 0;
     uint8_t *d_src = c.d_buf, *d_dst = d_src + src_b, *d_meta = d_dst + dst_b, *d_ws = d_meta + 256;
     Meta *m = (Meta *)c.h_meta;

@@ -39,6 +39,7 @@ __device__ int decode_block_lane(const uint8_t *src, uint32_t src_len, uint8_t *
         if (cw == 1) {
             if (ip + 4 > csize) return QLZX_E_CORRUPT;
             cw = ld_u32_bytes(src + ip);
+            if (!(cw >> 31)) return QLZX_E_CORRUPT;  // sentinel bit (quicklz.c:221)
             ip += 4;
         }
         if (ip >= csize) return QLZX_E_CORRUPT;

@@ -97,7 +97,7 @@ typedef struct qlzx_blocks {
  *                above the fast-path limit take the general kernel)
  * The record CRC is computed over the compressed bytes in the same pass that
  * decodes them (fused). */
-size_t qlzx_decompress_workspace_size(uint32_t n);
+size_t qlzx_decompress_workspace_size(uint32_t n, uint32_t max_dsize);
 int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_t *dsize,
                           int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
                           uint32_t *crc_out, uint32_t max_dsize, void *workspace,

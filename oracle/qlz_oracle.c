@@ -192,6 +192,7 @@ int orc_decompress(const uint8_t *src, size_t src_len, uint8_t *dst, size_t dst_
         if (cw == 1) {
             if (ip + 4 > csize) return ORC_E_CORRUPT;
             cw = ld32(src + ip);
+            if (!(cw >> 31)) return ORC_E_CORRUPT; /* encoder always sets the sentinel (quicklz.c:221) */
             ip += 4;
         }
         if (ip >= csize) return ORC_E_CORRUPT;
