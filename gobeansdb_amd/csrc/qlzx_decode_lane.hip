@@ -6,10 +6,10 @@
 // (global memory), so it serves blocks of any size, including BodyMax = 50 MiB
 // values (config/mc_config.go:7).
 //
-// Semantics: quicklz.c:496-672 (qlz_decompress_core) on valid streams,
-// bounds-checked like oracle/qlz_oracle.c:orc_decompress (QLZ_MEMORY_SAFE,
-// quicklz.c:519-657, made strict); header/size checks of CDecompressSafe
-// (cquicklz.go:84-101).
+// Semantics: quicklz.c:496-672 (qlz_decompress_core) on every stream the
+// encoder can produce; malformed streams are rejected by checks C1-C5 of
+// oracle/qlz_oracle.c:orc_decompress; header/size checks of
+// CDecompressSafe (cquicklz.go:84-101).
 // The record CRC (store/datafile.go:66-76) is continued over the compressed
 // bytes in the same kernel.
 #include "qlzx_device.h"
@@ -33,9 +33,11 @@ __device__ int decode_block_lane(const uint8_t *src, uint32_t src_len, uint8_t *
         dsize_out = dsize;
         return QLZX_OK;
     }
+    // checks C1-C5 of oracle/qlz_oracle.c:orc_decompress
     uint32_t ip = h.hdr, op = 0, cw = 1;
-    const int64_t lit_fast_end = (int64_t)dsize - 1 - QLZX_TAIL;
-    for (;;) {
+    bool tail = false;
+    const int64_t tail_from = (int64_t)dsize - 1 - QLZX_TAIL;
+    while (op < dsize) {
         if (cw == 1) {
             if (ip + 4 > csize) return QLZX_E_CORRUPT;
             cw = ld_u32_bytes(src + ip);
@@ -44,33 +46,27 @@ __device__ int decode_block_lane(const uint8_t *src, uint32_t src_len, uint8_t *
         }
         if (ip >= csize) return QLZX_E_CORRUPT;
         if (cw & 1u) {
-            cw >>= 1;
+            if (tail) return QLZX_E_CORRUPT;
             const uint32_t tl = token_bytes(src[ip]);
             if (ip + tl > csize) return QLZX_E_CORRUPT;
             uint32_t t = 0;
             for (uint32_t k = 0; k < tl; k++) t |= (uint32_t)src[ip + k] << (8 * k);
             uint32_t off, len;
             ip += decode_token(t, off, len);
-            if (off < 3 || off > op) return QLZX_E_CORRUPT;
-            if ((uint64_t)op + len + 4 > dsize) return QLZX_E_CORRUPT;
+            if (off < 3 || off > op || (uint64_t)op + len + 4 > dsize) return QLZX_E_CORRUPT;
             uint8_t *d = dst + op;
             const uint8_t *s = d - off;
             for (uint32_t i = 0; i < len; i++) d[i] = s[i];  // forward (overlapping) copy
             op += len;
-        } else if ((int64_t)op < lit_fast_end) {
-            dst[op++] = src[ip++];
-            cw >>= 1;
         } else {
-            while (op < dsize) {  // literal tail (quicklz.c:645-668)
-                if (cw == 1) { ip += 4; cw = 0x80000000u; }
-                if (ip >= csize) return QLZX_E_CORRUPT;
-                dst[op++] = src[ip++];
-                cw >>= 1;
-            }
-            dsize_out = dsize;
-            return QLZX_OK;
+            if ((int64_t)op >= tail_from) tail = true;  // tail loop (quicklz.c:645-668)
+            dst[op++] = src[ip++];
         }
+        cw >>= 1;
     }
+    if (!(ip == csize || (ip < h.hdr + 9 && csize == h.hdr + 9))) return QLZX_E_CORRUPT;
+    dsize_out = dsize;
+    return QLZX_OK;
 }
 
 // Handles blocks with dsize >= min_dsize (smaller ones belong to the fast path

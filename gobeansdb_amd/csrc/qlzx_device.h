@@ -24,6 +24,8 @@ namespace qlzx {
 extern __device__ uint32_t g_crc_table[256];
 // g_crc_x8n[k] = x^(8 * 2^k) mod P in reflected form, for CRC shift/combine.
 extern __device__ uint32_t g_crc_pow[64];
+// g_crc_slice8[k * 256 + b]: CRC of byte b followed by k zero bytes (slicing-by-8).
+extern __device__ uint32_t g_crc_slice8[8 * 256];
 
 constexpr uint32_t CRC_POLY = 0xEDB88320u;
 
@@ -65,6 +67,39 @@ __device__ __forceinline__ uint32_t crc_word(const uint32_t *tab, uint32_t c, ui
 __device__ __forceinline__ void load_crc_table(uint32_t *lds_tab) {
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) lds_tab[i] = g_crc_table[i];
 }
+
+// Slicing-by-8 update over 8 bytes (lo = bytes 0..3, hi = bytes 4..7), tables in LDS.
+__device__ __forceinline__ uint32_t crc_slice8(const uint32_t *t, uint32_t c, uint32_t lo, uint32_t hi) {
+    const uint32_t x = lo ^ c;
+    return t[7 * 256 + (x & 0xff)] ^ t[6 * 256 + ((x >> 8) & 0xff)] ^ t[5 * 256 + ((x >> 16) & 0xff)] ^
+           t[4 * 256 + (x >> 24)] ^ t[3 * 256 + (hi & 0xff)] ^ t[2 * 256 + ((hi >> 8) & 0xff)] ^
+           t[1 * 256 + ((hi >> 16) & 0xff)] ^ t[hi >> 24];
+}
+
+// LDS DMA (global -> LDS, no VGPR destination): each lane's bytes land at
+// lds_base + 16*lane (dwordx4) or + 4*lane (dword); lds_base must be
+// wave-uniform.  Issued as inline asm so the compiler's waitcnt pass does not
+// serialise later LDS reads behind it; callers wait with vm_sync()/vmcnt(N).
+// M0 is saved and restored around the DMA.
+__device__ __forceinline__ void dma16(const void *g, uint32_t lds_base) {
+    uint32_t tmp;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(tmp)
+                 : "s"(__builtin_amdgcn_readfirstlane(lds_base)), "v"(g)
+                 : "memory");
+}
+__device__ __forceinline__ void dma4(const void *g, uint32_t lds_base) {
+    uint32_t tmp;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tglobal_load_lds_dword %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(tmp)
+                 : "s"(__builtin_amdgcn_readfirstlane(lds_base)), "v"(g)
+                 : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
+
+// s_waitcnt on LDS only (no vmcnt), plus a compiler memory barrier.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void vm_sync() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
 __device__ __forceinline__ uint32_t ld_u32_bytes(const uint8_t *p) {

@@ -6,6 +6,7 @@ namespace qlzx {
 struct CrcTables {
     uint32_t table[256];
     uint32_t pow8[64];
+    uint32_t slice[8][256];  // slice[k][b]: CRC of byte b followed by k zero bytes (slicing-by-8)
 };
 
 __host__ __device__ constexpr uint32_t mulmod_c(uint32_t a, uint32_t b) {
@@ -25,6 +26,12 @@ __host__ __device__ constexpr CrcTables make_tables() {
         for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ CRC_POLY : (c >> 1);
         t.table[i] = c;
     }
+    for (uint32_t i = 0; i < 256; i++) t.slice[0][i] = t.table[i];
+    for (int k = 1; k < 8; k++)
+        for (uint32_t i = 0; i < 256; i++) {
+            const uint32_t c = t.slice[k - 1][i];
+            t.slice[k][i] = (c >> 8) ^ t.table[c & 0xffu];
+        }
     // x^1 in reflected form is bit 30; square 3 times -> x^8 (one byte of zeros)
     uint32_t x = 0x40000000u;
     for (int k = 0; k < 3; k++) x = mulmod_c(x, x);
@@ -47,6 +54,18 @@ __device__ uint32_t g_crc_table[256] = {
 #undef R64
 #undef R8
 #undef R
+};
+
+__device__ uint32_t g_crc_slice8[8 * 256] = {
+#define S(k, i) kTables.slice[k][i]
+#define S8(k, i) S(k, i), S(k, i + 1), S(k, i + 2), S(k, i + 3), S(k, i + 4), S(k, i + 5), S(k, i + 6), S(k, i + 7)
+#define S64(k, i) S8(k, i), S8(k, i + 8), S8(k, i + 16), S8(k, i + 24), S8(k, i + 32), S8(k, i + 40), S8(k, i + 48), S8(k, i + 56)
+#define S256(k) S64(k, 0), S64(k, 64), S64(k, 128), S64(k, 192)
+    S256(0), S256(1), S256(2), S256(3), S256(4), S256(5), S256(6), S256(7)
+#undef S256
+#undef S64
+#undef S8
+#undef S
 };
 
 __device__ uint32_t g_crc_pow[64] = {

@@ -164,13 +164,18 @@ size_t orc_compress(const uint8_t *src, size_t n, uint8_t *dst) { return compres
 size_t orc_compress_go(const uint8_t *src, size_t n, uint8_t *dst) { return compress_common(src, n, dst, 1); }
 
 /*
- * Level-3 decoder: quicklz.c:496-672 / quicklz.go:291-431, bounds-checked
- * in the spirit of QLZ_MEMORY_SAFE (quicklz.c:519-521,527-530,613-619,
- * 654-657): every byte read lies inside csize, match sources inside the
- * output produced so far, and match end + 4 <= dsize (computed without the
- * reference's unsigned wrap-around).  Unlike QLZ_MEMORY_SAFE's 4-byte
- * look-ahead, only the bytes a token occupies are required, so the short
- * streams Go's Compress emits for 1..4-byte inputs decode too.
+ * Level-3 decoder: quicklz.c:496-672 / quicklz.go:291-431.  On every stream
+ * qlz_compress (C or Go mode) can produce, the output equals the reference's.
+ * Malformed input -- undefined behaviour in the reference, which is built
+ * without QLZ_MEMORY_SAFE (quicklz.h:31) -- is rejected by these checks, which
+ * the HIP decoders implement identically:
+ *   C1 every control word is fully inside csize and has its sentinel bit 31
+ *   C2 every token / literal byte lies inside csize
+ *   C3 matches: 3 <= offset <= op and op + len + 4 <= dsize (quicklz.c:613-619)
+ *   C4 after the first literal at op >= dsize-11 (the tail loop of
+ *      quicklz.c:645-668) every further item is a literal
+ *   C5 the stream ends with the item that completes dsize, except for the
+ *      zero padding up to the 9-byte core minimum (quicklz.c:493)
  */
 int orc_decompress(const uint8_t *src, size_t src_len, uint8_t *dst, size_t dst_cap, size_t *out_len) {
     if (src_len < 3) return ORC_E_HEADER;
@@ -188,46 +193,41 @@ int orc_decompress(const uint8_t *src, size_t src_len, uint8_t *dst, size_t dst_
     }
     size_t ip = hdr, op = 0;
     uint32_t cw = 1;
-    for (;;) {
+    int tail = 0;
+    while (op < dsize) {
         if (cw == 1) {
-            if (ip + 4 > csize) return ORC_E_CORRUPT;
+            if (ip + 4 > csize) return ORC_E_CORRUPT;                       /* C1 */
             cw = ld32(src + ip);
-            if (!(cw >> 31)) return ORC_E_CORRUPT; /* encoder always sets the sentinel (quicklz.c:221) */
+            if (!(cw >> 31)) return ORC_E_CORRUPT;                          /* C1 */
             ip += 4;
         }
-        if (ip >= csize) return ORC_E_CORRUPT;
+        if (ip >= csize) return ORC_E_CORRUPT;                              /* C2 */
         if (cw & 1u) {
-            /* bounds: every byte the token occupies must lie inside csize */
+            if (tail) return ORC_E_CORRUPT;                                 /* C4 */
             const uint32_t b0 = src[ip];
             const uint32_t tl = (b0 & 3) == 0 ? 1 : (b0 & 3) != 3 ? 2 : (b0 & 127) != 3 ? 3 : 4;
-            if (ip + tl > csize) return ORC_E_CORRUPT;
+            if (ip + tl > csize) return ORC_E_CORRUPT;                      /* C2 */
             uint32_t t = 0;
             for (uint32_t k = 0; k < tl; k++) t |= (uint32_t)src[ip + k] << (8 * k);
             uint32_t off, ml;
-            cw >>= 1;
-            if ((t & 3) == 0) { off = (t & 0xff) >> 2; ml = 3; ip += 1; }
-            else if ((t & 2) == 0) { off = (t & 0xffff) >> 2; ml = 3; ip += 2; }
-            else if ((t & 1) == 0) { off = (t & 0xffff) >> 6; ml = ((t >> 2) & 15) + 3; ip += 2; }
-            else if ((t & 127) != 3) { off = (t >> 7) & 0x1ffff; ml = ((t >> 2) & 0x1f) + 2; ip += 3; }
-            else { off = t >> 15; ml = ((t >> 7) & 255) + 3; ip += 4; }
-            if (off < 3 || off > op) return ORC_E_CORRUPT;
-            if ((size_t)op + ml + 4 > dsize) return ORC_E_CORRUPT;
-            for (uint32_t i = 0; i < ml; i++) dst[op + i] = dst[op - off + i]; /* forward copy */
+            if ((t & 3) == 0) { off = (t & 0xff) >> 2; ml = 3; }
+            else if ((t & 2) == 0) { off = (t & 0xffff) >> 2; ml = 3; }
+            else if ((t & 1) == 0) { off = (t & 0xffff) >> 6; ml = ((t >> 2) & 15) + 3; }
+            else if ((t & 127) != 3) { off = (t >> 7) & 0x1ffff; ml = ((t >> 2) & 0x1f) + 2; }
+            else { off = t >> 15; ml = ((t >> 7) & 255) + 3; }
+            ip += tl;
+            if (off < 3 || off > op || op + ml + 4 > dsize) return ORC_E_CORRUPT;  /* C3 */
+            for (uint32_t i = 0; i < ml; i++) dst[op + i] = dst[op - off + i];   /* forward copy */
             op += ml;
-        } else if ((long long)op < (long long)dsize - 1 - TAIL_LITERALS) {
-            dst[op++] = src[ip++];
-            cw >>= 1;
         } else {
-            while (op < dsize) {
-                if (cw == 1) { ip += 4; cw = 0x80000000u; }
-                if (ip >= csize) return ORC_E_CORRUPT;
-                dst[op++] = src[ip++];
-                cw >>= 1;
-            }
-            *out_len = dsize;
-            return ORC_OK;
+            if ((long long)op >= (long long)dsize - 1 - TAIL_LITERALS) tail = 1;
+            dst[op++] = src[ip++];
         }
+        cw >>= 1;
     }
+    if (!(ip == csize || (ip < hdr + 9 && csize == hdr + 9))) return ORC_E_CORRUPT;  /* C5 */
+    *out_len = dsize;
+    return ORC_OK;
 }
 
 /* CRC-32/IEEE reflected table (poly 0xEDB88320), as store/crc32.go:5-59 */
