@@ -13,7 +13,7 @@ import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libqlzx.so")
+LIB_PATH = os.environ.get("QLZX_LIB", os.path.join(HERE, "libqlzx.so"))
 HEADER = os.path.join(ROOT, "include", "qlzx.h")
 
 # enum qlzx_status

@@ -21,19 +21,28 @@ def _stale() -> bool:
     return any(os.path.getmtime(s) > t for s in srcs)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
-        return OUT
+PROF_OUT = os.path.join(HERE, "libqlzx_prof.so")
+
+
+def _compile(out: str, extra: list[str], verbose: bool) -> None:
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-Wno-unused-parameter",
-           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp",
+           "-Wall", "-Wno-unused-function", "-Wno-unused-parameter", *extra,
+           "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp",
            os.path.join(CSRC, "qlzx_api.hip")]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
+    os.replace(out + ".tmp", out)
+
+
+def build(force: bool = False, verbose: bool = False, profile: bool = False) -> str:
+    """libqlzx.so (release) and, with profile=True, libqlzx_prof.so (phase stamps)."""
+    if force or _stale():
+        _compile(OUT, [], verbose)
+    if profile:
+        _compile(PROF_OUT, ["-DQLZX_PROFILE"], verbose)
     return OUT
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, profile="--profile" in sys.argv))

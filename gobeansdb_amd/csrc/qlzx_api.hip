@@ -46,6 +46,15 @@ constexpr uint32_t kMaxLaneSlabs = 4096;  // concurrent lane encoders for the ge
 
 }  // namespace
 
+#ifdef QLZX_PROFILE
+namespace qlzx {
+__device__ unsigned long long *g_prof = nullptr;
+}
+extern "C" int qlzx_profile_set(void *dev_buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(qlzx::g_prof), &dev_buf, sizeof(void *));
+}
+#endif
+
 extern "C" {
 
 const char *qlzx_last_error(void) { return t_last_error.c_str(); }

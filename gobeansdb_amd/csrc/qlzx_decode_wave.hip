@@ -47,11 +47,13 @@ struct GroupRec {
 
 constexpr int32_t kPending = -1;  // status of blocks left to the general path
 constexpr uint32_t kBlkSkip = 0, kBlkStored = 1, kBlkCompressed = 2;
-constexpr uint32_t kParseWG = 256;
+constexpr uint32_t kParseWG = 64;          // K1 workgroup: one wave (LDS per wave bounds occupancy)
 constexpr uint32_t kChunkBlocks = 131072;  // >= 256 CUs x 8 waves x 64 lanes: K1 fills the chip
 constexpr uint32_t kRoundBytes = 64;          // bytes DMA'd per lane per round (4 x 16 B)
-constexpr uint32_t kRingSlots = 4;            // rounds resident per lane: r-1, r, r+1, r+2 (issuing)
-constexpr uint32_t kRingWave = kRingSlots * kRoundBytes * 64;  // 16 KiB per wave
+constexpr uint32_t kRingSlots = 3;            // rounds resident per lane: r, r+1 (landing), r+2 (issuing)
+constexpr uint32_t kRingWave = kRingSlots * kRoundBytes * 64;  // 12 KiB per wave
+constexpr uint32_t kTokSlots = 4;  // K2 token prefetch slots (batch % 4)
+constexpr uint32_t kRecSlots = 7;  // K2 group-record prefetch slots (batch % 7)
 
 __host__ __device__ inline uint32_t groups_max(uint32_t max_dsize) { return max_dsize / 31u + 2u; }
 
@@ -66,10 +68,10 @@ inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
 
 // ------------------------------------------------------------------ K1 ----
 // Ring layout per wave: [slot][piece 0..3][lane][16 B]; stream byte p of a lane
-// (q = p + shift, shift = src & 15) lives in round q/64, slot (q/64) % 4,
+// (q = p + shift, shift = src & 15) lives in round q/64, slot (q/64) % 3,
 // piece (q/16) % 4, byte q % 16.
 __device__ __forceinline__ uint32_t ring_off(uint32_t q, uint32_t lane) {
-    return ((((q >> 6) & (kRingSlots - 1)) * 4 + ((q >> 4) & 3)) * 64 + lane) * 16 + (q & 15);
+    return ((((q >> 6) % kRingSlots) * 4 + ((q >> 4) & 3)) * 64 + lane) * 16 + (q & 15);
 }
 __device__ __forceinline__ uint32_t ring_rd32(const uint8_t *ring, uint32_t q, uint32_t lane) {
     const uint32_t qa = q & ~3u;
@@ -88,7 +90,7 @@ __device__ __forceinline__ void ring_issue(uint8_t *ring_wave, const uint8_t *gb
     for (uint32_t j = 0; j < 4; j++) {
         const uint32_t c16 = r * 4 + j;
         const uint8_t *g = (active && c16 <= last16) ? gbase + (size_t)c16 * 16 : dummy;
-        dma16(g, lds_addr(ring_wave + ((r & (kRingSlots - 1)) * 4 + j) * 1024));
+        dma16(g, lds_addr(ring_wave + ((r % kRingSlots) * 4 + j) * 1024));
     }
 }
 
@@ -150,13 +152,16 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
     uint32_t crc = (CRC && inrange && crc_state) ? crc_state[i] : 0xffffffffu;
     bool done_parse = !parsing;
 
+    PROF_DECL
     const uint8_t *dummy = (const uint8_t *)(((uintptr_t)b.src) & ~(uintptr_t)15);
     ring_issue(ring, gbase, dummy, 0, last16, stream);
     ring_issue(ring, gbase, dummy, 1, last16, stream && last_round >= 1);
     for (uint32_t r = 0;; r++) {
         if (__ballot(stream && r <= last_round) == 0) break;
         // rounds <= r landed once at most the newest round's 4 DMAs are in flight
+        PROF_MARK(0);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        PROF_MARK(1);  // 1: waiting for the round's DMA
         const bool act = stream && r <= last_round;
         if (CRC && act) {  // CRC of this round's bytes, in stream order
             const uint32_t q0 = r * kRoundBytes, q1 = q0 + kRoundBytes;
@@ -171,46 +176,59 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
             }
             while (q < hi) { crc = crc_byte(tab, crc, ring[ring_off(q, lane)]); q++; }
         }
+        PROF_MARK(2);  // 2: CRC
         // parse while the bytes the next step reads have landed (stream pos < lim)
         const uint32_t lim = (r + 1) * kRoundBytes - shift;
         bool go = act && !done_parse;
         while (__ballot(go)) {
-            if (!go) continue;
-            if (k == 31) {  // group boundary: control word (quicklz.c:517-525)
-                if (ip + 4 > csize) { done_parse = true; go = false; continue; }  // stream ends
-                if (ip + 4 > lim) { go = false; continue; }
-                if (g > 0) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
-                if (g >= gmax) { st = QLZX_E_CORRUPT; done_parse = true; go = false; continue; }
-                rec_ip = ip;
-                cw = ring_rd32(ring, ip + shift, lane);
-                if (!(cw >> 31)) { st = QLZX_E_CORRUPT; done_parse = true; go = false; continue; }  // C1
-                ip += 4;
-                k = 0; m = 0; ra = 0; rb = 0;
-                g++;
-                continue;
+#ifdef QLZX_PROFILE
+            _pacc[5] += 1;
+            if (go) _pacc[6] += 1;
+#endif
+            // one step = a control word (k == 31) or one item: a match token or a
+            // literal run.  Straight-line selects; only the record store branches.
+            const bool gb = k == 31;
+            const uint32_t bit = gb ? 0u : ((cw >> k) & 1u);
+            const uint32_t need = gb ? 4u : bit;          // bytes this step reads at ip
+            const bool end = gb ? (ip + 4 > csize) : (ip >= csize);
+            const bool wait = !end && ip + need > lim;
+            const bool stepping = go && !end && !wait;
+            const uint32_t w = ring_rd32(ring, ip + shift, lane);  // cword or token (unused for literals)
+            const uint32_t code = ((w & 3u) == 0) ? 0u : ((w & 3u) != 3u) ? 1u : ((w & 127u) != 3u) ? 2u : 3u;
+            uint32_t run = __builtin_ctz((cw >> (k & 31)) | (1u << (31 - (k & 31))));
+            if (run > csize - ip) run = csize - ip;
+            const bool rec_out = stepping && gb && g > 0;
+            const GroupRec prev{rec_ip, m, ra, rb};
+            if (rec_out) myrec[g - 1] = prev;
+            const bool sentinel_bad = stepping && gb && !(w >> 31);
+            const bool trunc_bad = stepping && bit && ip + code + 1 > csize;
+            const bool gmax_bad = stepping && gb && g >= gmax;
+            if (sentinel_bad || trunc_bad || gmax_bad) st = QLZX_E_CORRUPT;  // C1 / C2 / C5
+            const bool bad = sentinel_bad || trunc_bad || gmax_bad;
+            const bool adv = stepping && !bad;
+            const uint32_t kk = k & 31;
+            if (adv) {
+                if (gb) {
+                    rec_ip = ip; cw = w; ip += 4; k = 0; m = 0; ra = 0; rb = 0; g++;
+                } else {
+                    m |= bit << kk;
+                    ra |= (bit & code) << kk;
+                    rb |= (bit & (code >> 1)) << kk;
+                    ip += bit ? code + 1 : run;
+                    k += bit ? 1u : run;
+                }
             }
-            if (ip >= csize) { done_parse = true; go = false; continue; }
-            if ((cw >> k) & 1u) {  // match: only the token's first byte (its length) is needed
-                if (ip + 1 > lim) { go = false; continue; }
-                const uint32_t tl = token_bytes(ring[ring_off(ip + shift, lane)]);
-                if (ip + tl > csize) { st = QLZX_E_CORRUPT; done_parse = true; go = false; continue; }  // C2/C5
-                m |= 1u << k;
-                ra |= ((tl - 1) & 1u) << k;
-                rb |= ((tl - 1) >> 1) << k;
-                ip += tl;
-                k++;
-            } else {  // literal run to the next match bit or the group end (no bytes read)
-                uint32_t run = __builtin_ctz((cw >> k) | (1u << (31 - k)));
-                if (run > csize - ip) run = csize - ip;
-                ip += run;
-                k += run;
-            }
+            if (go && (end || bad)) done_parse = true;
+            go = adv;
         }
+        PROF_MARK(3);  // 3: parse
         if (!CRC && done_parse) stream = false;  // nothing left to read for this lane
         // round r+2 reuses the slot of round r-2 (consumed: every lane is past 64 (r-1))
         ring_issue(ring, gbase, dummy, r + 2, last16, stream && r + 2 <= last_round);
     }
+    PROF_MARK(4);  // 4: DMA issue + loop overhead
     if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
+    PROF_FLUSH(0);
     vm_sync();
     if (!inrange) return;
     if (st == QLZX_OK && kind == kBlkCompressed && (!done_parse || g == 0)) st = QLZX_E_CORRUPT;
@@ -249,57 +267,82 @@ __device__ __forceinline__ void lds_mskor(uint32_t *addr, uint32_t mask, uint32_
     asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(a), "v"(mask), "v"(val) : "memory");
 }
 
-// Store n (1..16) bytes held in w[0..3] at LDS byte q; bytes outside [q, q+n) untouched.
-__device__ __forceinline__ void lds_put16(uint8_t *out, uint32_t q, const uint32_t w[4], uint32_t n) {
-    const uint32_t qa = q & 3u;
-    uint32_t *d = (uint32_t *)(out + (q & ~3u));
-    uint32_t o[5];
-    o[0] = w[0] << (8 * qa);
-    o[1] = qa ? __builtin_amdgcn_alignbyte(w[1], w[0], 4 - qa) : w[1];
-    o[2] = qa ? __builtin_amdgcn_alignbyte(w[2], w[1], 4 - qa) : w[2];
-    o[3] = qa ? __builtin_amdgcn_alignbyte(w[3], w[2], 4 - qa) : w[3];
-    o[4] = qa ? (w[3] >> (8 * (4 - qa))) : 0u;
-    const uint32_t end = qa + n;
-#pragma unroll
-    for (uint32_t j = 0; j < 5; j++) {
-        const int lo = (int)qa - (int)(4 * j), hi = (int)end - (int)(4 * j);
-        const uint32_t blo = lo < 0 ? 0u : (lo > 4 ? 4u : (uint32_t)lo);
-        const uint32_t bhi = hi < 0 ? 0u : (hi > 4 ? 4u : (uint32_t)hi);
-        if (bhi > blo) {
-            const uint32_t mask = (bhi == 4 ? 0xffffffffu : ((1u << (8 * bhi)) - 1u)) & ~((1u << (8 * blo)) - 1u);
-            if (mask == 0xffffffffu) d[j] = o[j];
-            else lds_mskor(d + j, mask, o[j] & mask);
-        }
-    }
-}
-
 template <uint32_t MAXD>
 struct K2Lds {
+    uint8_t front[16];       // lets a match's first source dword start up to 4 B before out[0]
     uint8_t out[MAXD + 32];
-    GroupRec rec[3][64];     // per-lane group record of batches b, b+1, b+2 (slot = batch % 3)
-    uint32_t tok[2][2][64];  // per-lane token dwords (lo, hi) of batches b, b+1 (slot = batch % 2)
+    uint32_t tok[kTokSlots][64];     // per-lane token dword of batches b..b+3
+    GroupRec rec[kRecSlots][4];      // records of the <= 4 groups of batches b..b+6
 };
 
-// DMA the group record of item I = 64 bt + lane into rec slot bt % 3.
-__device__ __forceinline__ void issue_rec(GroupRec (*rec)[64], const GroupRec *rb, uint32_t bt, uint32_t nitems,
+// Every K2 iteration issues exactly 2 DMA instructions (1 token dword + 1
+// record), with dummy addresses for lanes/batches past the end, so that
+// "s_waitcnt vmcnt(4)" at the end of iteration bt means "everything issued up
+// to iteration bt-2 has landed".  Iteration bt issues the tokens of bt+3 and
+// the records of bt+6, so both have two whole iterations to arrive.
+__device__ __forceinline__ void issue_rec(GroupRec (*rec)[4], const GroupRec *rb, uint32_t bt, uint32_t ngroups,
                                           uint32_t lane) {
-    const uint32_t I = bt * 64 + lane;
-    if (I < nitems) dma16(rb + I / 31, lds_addr(&rec[bt % 3][0]));
+    const uint32_t g = (bt * 64) / 31 + lane;
+    if (lane < 4) dma16(g < ngroups ? (const void *)(rb + g) : (const void *)rb, lds_addr(&rec[bt % kRecSlots][0]));
 }
-
-// From the landed record of batch bt, DMA the two dwords holding item bytes [pos, pos+4).
-__device__ __forceinline__ void issue_tok(const GroupRec *recslot, uint32_t (*tok)[64], const uint8_t *src,
+// Item position: cword at gr.ip, then k items of which popc(a)+2popc(b) extra token bytes.
+__device__ __forceinline__ uint32_t item_pos(const GroupRec &gr, uint32_t k) {
+    const uint32_t low = (1u << k) - 1u;
+    return gr.ip + 4 + k + __builtin_popcount(gr.a & low) + 2 * __builtin_popcount(gr.b & low);
+}
+// The 4 stream bytes at min(pos, csize - 4) (unaligned dword DMA; csize >= 7
+// for a compressed level-3 stream, so the read stays inside the block).
+__device__ __forceinline__ void issue_tok(const GroupRec *recslot, uint32_t *tok, const uint8_t *src,
                                           uint32_t csize, uint32_t bt, uint32_t nitems, uint32_t lane) {
     const uint32_t I = bt * 64 + lane;
+    uint32_t p = 0;
     if (I < nitems) {
-        const GroupRec gr = recslot[lane];
-        const uint32_t k = I - (I / 31) * 31, low = (1u << k) - 1u;
-        const uint32_t pos = gr.ip + 4 + k + __builtin_popcount(gr.a & low) + 2 * __builtin_popcount(gr.b & low);
-        const uintptr_t aa = ((uintptr_t)(src + pos)) & ~(uintptr_t)3;
-        dma4((const void *)aa, lds_addr(&tok[0][0]));
-        if (aa + 4 < (uintptr_t)(src + csize)) dma4((const void *)(aa + 4), lds_addr(&tok[1][0]));
+        const uint32_t g = I / 31;
+        p = item_pos(recslot[g - (bt * 64) / 31], I - g * 31);
+        p = p + 4 <= csize ? p : csize - 4;
     }
+    dma4(src + p, lds_addr(tok));
 }
+
+// Byte mask of bytes [lo, hi) of one dword (lo, hi clamped to [0, 4]).
+__device__ __forceinline__ uint32_t dw_mask(int lo, int hi) {
+    lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
+    hi = hi < 0 ? 0 : (hi > 4 ? 4 : hi);
+    if (hi <= lo) return 0u;
+    const uint32_t h = hi == 4 ? 0xffffffffu : ((1u << (8 * hi)) - 1u);
+    return h & ~((1u << (8 * lo)) - 1u);
+}
+
+// One 16-byte copy step, prepared once per batch: destination dword j (at
+// qa + 4j) takes the source bytes at qa + 4j - off, i.e. alignbyte(x[j+1], x[j], sh)
+// over the aligned source dwords x[] starting at xa.
+struct Copy16 {
+    uint32_t qa, mk[5];
+    int xa;
+    uint32_t sh;
+    __device__ __forceinline__ void prep(uint32_t q, uint32_t off, uint32_t n) {
+        qa = q & ~3u;
+        const int sa = (int)qa - (int)off;  // >= -4: out[] has a 16-B front pad
+        xa = sa & ~3;
+        sh = (uint32_t)sa & 3u;
+        const int lo = (int)(q & 3u), hi = lo + (int)n;
+        mk[0] = dw_mask(lo, hi);
+        mk[1] = dw_mask(lo - 4, hi - 4);
+        mk[2] = dw_mask(lo - 8, hi - 8);
+        mk[3] = dw_mask(lo - 12, hi - 12);
+        mk[4] = dw_mask(lo - 16, hi - 16);
+    }
+    __device__ __forceinline__ void run(uint8_t *out) const {
+        const uint32_t *x = (const uint32_t *)(out + xa);
+        const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4], x5 = x[5];
+        uint32_t *dw = (uint32_t *)(out + qa);
+        if (mk[0]) lds_mskor(dw + 0, mk[0], __builtin_amdgcn_alignbyte(x1, x0, sh) & mk[0]);
+        if (mk[1]) lds_mskor(dw + 1, mk[1], __builtin_amdgcn_alignbyte(x2, x1, sh) & mk[1]);
+        if (mk[2]) lds_mskor(dw + 2, mk[2], __builtin_amdgcn_alignbyte(x3, x2, sh) & mk[2]);
+        if (mk[3]) lds_mskor(dw + 3, mk[3], __builtin_amdgcn_alignbyte(x4, x3, sh) & mk[3]);
+        if (mk[4]) lds_mskor(dw + 4, mk[4], __builtin_amdgcn_alignbyte(x5, x4, sh) & mk[4]);
+    }
+};
 
 // Inclusive prefix sum over the 64 lanes with DPP (row shifts + row broadcasts).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -334,34 +377,36 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
     }
     uint8_t *out = L.out;
     const GroupRec *rb = recs + (size_t)li * gmax;
-    const uint32_t nitems = bi.nitems;
+    const uint32_t nitems = bi.nitems, ngroups = bi.ngroups;
     const uint32_t csize = b.src_len[i];
     const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
     const uint32_t nb = (nitems + 63) / 64;
     const uint32_t tail_from = dsize > QLZX_TAIL ? dsize - 1 - QLZX_TAIL : 0;  // op >= this: tail (quicklz.c:503)
-    // prologue: records of batches 0 and 1, then the tokens of batch 0
-    issue_rec(L.rec, rb, 0, nitems, lane);
-    issue_rec(L.rec, rb, 1, nitems, lane);
+    // prologue: records of batches 0..5, then the tokens of batches 0..2
+    for (uint32_t j = 0; j < 6; j++) issue_rec(L.rec, rb, j, ngroups, lane);
     vm_sync();
-    issue_tok(L.rec[0], L.tok[0], src, csize, 0, nitems, lane);
+    for (uint32_t j = 0; j < 3; j++) issue_tok(L.rec[j], L.tok[j], src, csize, j, nitems, lane);
     vm_sync();
+    PROF_DECL
     uint32_t D = 0;
     bool bad = false, tail = false, complete = dsize == 0;
     for (uint32_t bt = 0; bt < nb && !complete && !bad; bt++) {
-        // invariant: rec[bt], rec[bt+1], tok[bt] landed.  Read this batch's state first.
+        // invariant: tok[bt..bt+2] and rec[bt..bt+5] landed.  Read this batch's state first.
         const uint32_t I = bt * 64 + lane;
         const bool valid = I < nitems;
-        const GroupRec gr = L.rec[bt % 3][lane];
-        const uint32_t tlo = L.tok[bt & 1][0][lane], thi = L.tok[bt & 1][1][lane];
+        const uint32_t g = I / 31;
+        const GroupRec gr = L.rec[bt % kRecSlots][valid ? g - (bt * 64) / 31 : 0];
+        const uint32_t tw = L.tok[bt % kTokSlots][lane];
         lds_sync();
-        // prefetch: tokens of bt+1 (its records landed), records of bt+2
-        if (bt + 1 < nb) issue_tok(L.rec[(bt + 1) % 3], L.tok[(bt + 1) & 1], src, csize, bt + 1, nitems, lane);
-        if (bt + 2 < nb) issue_rec(L.rec, rb, bt + 2, nitems, lane);
-
-        const uint32_t k = I - (I / 31) * 31, low = (1u << k) - 1u;
+        PROF_MARK(0);  // 0: batch state reads
+        // prefetch: tokens of bt+3 (its records landed), records of bt+6
+        issue_tok(L.rec[(bt + 3) % kRecSlots], L.tok[(bt + 3) % kTokSlots], src, csize, bt + 3, nitems, lane);
+        issue_rec(L.rec, rb, bt + 6, ngroups, lane);
+        PROF_MARK(1);  // 1: prefetch issue
+        const uint32_t k = I - g * 31;
         const bool is_match = valid && ((gr.m >> k) & 1u);
-        const uint32_t pos = gr.ip + 4 + k + __builtin_popcount(gr.a & low) + 2 * __builtin_popcount(gr.b & low);
-        const uint32_t t = __builtin_amdgcn_alignbyte(thi, tlo, (uint32_t)(((uintptr_t)(src + pos)) & 3u));
+        const uint32_t pos = item_pos(gr, k);
+        const uint32_t t = pos + 4 <= csize ? tw : tw >> (8 * (pos + 4 - csize));
         uint32_t off = 0, len = valid ? 1u : 0u, tl = 1;
         if (is_match) tl = decode_token(t, off, len);
         const uint32_t incl = wave_incl_scan(len);
@@ -369,8 +414,7 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
         const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
         // ---- checks C2-C5 on the live items (those that start before dsize) ----
         const bool live = valid && d < dsize;
-        const bool lit_tail = live && !is_match && d >= tail_from;
-        const uint64_t tail_lanes = __ballot(lit_tail);
+        const uint64_t tail_lanes = __ballot(live && !is_match && d >= tail_from);
         const uint32_t tail_lane = tail ? 0u : (tail_lanes ? (uint32_t)__builtin_ctzll(tail_lanes) : 64u);  // C4
         bool ok = true;
         if (live && is_match)  // C3, and C4: no match after the first tail literal
@@ -382,17 +426,33 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
         if (__ballot(live && !ok)) { bad = true; break; }
         tail = tail || tail_lanes != 0;
         complete = __ballot(live && d + len == dsize) != 0;
+        PROF_MARK(2);  // 2: decode + scan + checks
         if (live && !is_match) out[d] = (uint8_t)t;
-        bool done = !(live && is_match);
+        // ---- matches: copy in sub-rounds ----
+        const bool mlive = live && is_match;
+        bool done = !mlive;
         const uint32_t s = d - off;
         const uint32_t send = (s + len < d) ? s + len : d;
+        const uint32_t end = d + len;
         const bool bytewise = off < 16 && off < len;
+        Copy16 cp;
+        cp.prep(d, off, len < 16 ? len : 16);
         for (;;) {
             lds_sync();
-            const uint64_t pend = __ballot(!done);
+            uint64_t pend = __ballot(!done);
             if (!pend) break;
-            const uint32_t du = __builtin_amdgcn_readlane(d, (uint32_t)__builtin_ctzll(pend));
-            if (!done && send <= du) {
+            // the first three pending matches bound three gaps whose bytes are all final
+            const uint32_t u0 = (uint32_t)__builtin_ctzll(pend);
+            pend &= pend - 1;
+            const uint32_t u1 = pend ? (uint32_t)__builtin_ctzll(pend) : u0;
+            pend &= pend - 1;
+            const uint32_t u2 = pend ? (uint32_t)__builtin_ctzll(pend) : u1;
+            const uint32_t d0 = __builtin_amdgcn_readlane(d, u0), e0 = __builtin_amdgcn_readlane(end, u0);
+            const uint32_t d1 = u1 != u0 ? __builtin_amdgcn_readlane(d, u1) : 0xffffffffu;
+            const uint32_t e1 = __builtin_amdgcn_readlane(end, u1);
+            const uint32_t d2 = u2 != u1 ? __builtin_amdgcn_readlane(d, u2) : 0xffffffffu;
+            const bool ready = !done && (send <= d0 || (s >= e0 && send <= d1) || (u1 != u0 && s >= e1 && send <= d2));
+            if (ready) {
                 if (bytewise) {
                     uint32_t j2 = 0;
                     for (uint32_t j = 0; j < len; j++) {
@@ -400,18 +460,21 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
                         j2 = (j2 + 1 == off) ? 0 : j2 + 1;
                     }
                 } else {
-                    for (uint32_t c = 0; c < len; c += 16) {
-                        uint32_t w[4];
-                        lds_get16(out, s + c, w);
-                        lds_put16(out, d + c, w, len - c < 16 ? len - c : 16);
+                    cp.run(out);
+                    for (uint32_t c = 16; c < len; c += 16) {  // long matches, chunk by chunk
                         if (off < len) lds_sync();
+                        Copy16 c2;
+                        c2.prep(d + c, off, len - c < 16 ? len - c : 16);
+                        c2.run(out);
                     }
                 }
                 done = true;
             }
         }
+        PROF_MARK(3);  // 3: match sub-rounds
         D += total;
-        vm_sync();  // prefetches of bt+1 / bt+2 landed (issued before the resolve)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // DMAs of iterations <= bt-1 landed
+        PROF_MARK(4);  // 4: waiting for prefetch
     }
     vm_sync();
     lds_sync();
@@ -429,6 +492,8 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
             for (uint32_t q = p; q < e; q++) dst[q] = out[q];
         }
     }
+    PROF_MARK(5);  // 5: write-out
+    PROF_FLUSH(1);
     if (lane == 0) {
         status[i] = QLZX_OK;
         if (dsize_out) dsize_out[i] = dsize;

@@ -97,6 +97,33 @@ __device__ __forceinline__ void dma4(const void *g, uint32_t lds_base) {
 }
 __device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
 
+// ---- optional in-kernel phase timing (profiling build: -DQLZX_PROFILE) ----
+// Stamps are s_memtime (shader clock) deltas summed per phase into a debug
+// buffer; they never feed any output.  Release builds compile them away.
+#ifdef QLZX_PROFILE
+extern __device__ unsigned long long *g_prof;
+#define PROF_DECL unsigned long long _pt = __builtin_amdgcn_s_memtime(), _pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PROF_MARK(ph)                                             \
+    do {                                                          \
+        const unsigned long long _n = __builtin_amdgcn_s_memtime(); \
+        _pacc[ph] += _n - _pt;                                    \
+        _pt = _n;                                                 \
+    } while (0)
+#define PROF_FLUSH(slot)                                                            \
+    do {                                                                            \
+        if (g_prof && (threadIdx.x & 63) == 0)                                      \
+            for (int _j = 0; _j < 8; _j++) atomicAdd(&g_prof[(slot) * 8 + _j], _pacc[_j]); \
+    } while (0)
+#else
+#define PROF_DECL
+#define PROF_MARK(ph) \
+    do {              \
+    } while (0)
+#define PROF_FLUSH(slot) \
+    do {                 \
+    } while (0)
+#endif
+
 // s_waitcnt on LDS only (no vmcnt), plus a compiler memory barrier.
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void vm_sync() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }

@@ -1,0 +1,52 @@
+"""Phase timing of the fast decode kernels from the -DQLZX_PROFILE build (s_memtime stamps).
+
+usage: QLZX_LIB=gobeansdb_amd/libqlzx_prof.so python tools/phase_prof.py [nblocks] [block_size]
+"""
+import ctypes
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from gobeansdb_amd import _lib, batch
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 131072
+bs = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
+kind = sys.argv[3] if len(sys.argv) > 3 else "text"
+L = _lib.lib()
+L.qlzx_profile_set.argtypes = [ctypes.c_void_p]
+dev = torch.device("cuda")
+uniq = min(n, 16384)
+plain = batch.synth(kind, 7, [bs] * uniq, device=dev)
+comp, cs, st, _ = batch.compress(plain, max_len=bs)
+torch.cuda.synchronize()
+idx = np.arange(n) % uniq
+src = batch.BlockBatch(comp.data, comp.off[torch.from_numpy(idx).to(dev)], cs[torch.from_numpy(idx).to(dev)])
+out = batch.BlockBatch.empty_for([bs] * n, device=dev)
+ws = batch.Workspace(dev)
+batch.decompress(src, out, max_dsize=bs, workspace=ws)
+torch.cuda.synchronize()
+prof = torch.zeros(16, dtype=torch.int64, device=dev)
+assert L.qlzx_profile_set(prof.data_ptr()) == 0
+t0 = time.time()
+dsz, st, _ = batch.decompress(src, out, max_dsize=bs, workspace=ws)
+torch.cuda.synchronize()
+t1 = time.time()
+assert int((st != 0).sum()) == 0
+p = prof.cpu().numpy().astype(np.float64)
+csum = float(cs[torch.from_numpy(idx).to(dev)].double().sum())
+items_est = n * 3817
+waves_k1 = (n + 63) // 64
+rounds = csum / n / 64
+batches = n * 3817 / 64
+print(f"blocks {n} x {bs} {kind}: wall {1e3 * (t1 - t0):.2f} ms, ratio {csum / (n * bs):.3f}")
+names1 = ["pre-loop", "wait DMA", "CRC", "parse", "issue+end"]
+print("K1 per wave per round (cycles):", {nm: round(p[j] / waves_k1 / rounds) for j, nm in enumerate(names1)})
+print("K1 parse iterations per wave-round: %.1f, active lanes per iteration (lane 0 only sampled): %.2f"
+      % (p[5] / waves_k1 / rounds, p[6] / max(p[5], 1)))
+names2 = ["state reads", "prefetch issue", "decode+scan+checks", "sub-rounds", "wait prefetch", "write-out"]
+print("K2 per batch (cycles):", {nm: round(p[8 + j] / batches) for j, nm in enumerate(names2)})
+print("K2 per block total (cycles):", round(p[8:14].sum() / n))
