@@ -50,10 +50,16 @@ constexpr uint32_t kBlkSkip = 0, kBlkStored = 1, kBlkCompressed = 2;
 constexpr uint32_t kParseWG = 64;          // K1 workgroup: one wave (LDS per wave bounds occupancy)
 constexpr uint32_t kChunkBlocks = 131072;  // >= 256 CUs x 8 waves x 64 lanes: K1 fills the chip
 constexpr uint32_t kRoundBytes = 64;          // bytes DMA'd per lane per round (4 x 16 B)
-constexpr uint32_t kRingSlots = 3;            // rounds resident per lane: r, r+1 (landing), r+2 (issuing)
-constexpr uint32_t kRingWave = kRingSlots * kRoundBytes * 64;  // 12 KiB per wave
-constexpr uint32_t kTokSlots = 4;  // K2 token prefetch slots (batch % 4)
-constexpr uint32_t kRecSlots = 7;  // K2 group-record prefetch slots (batch % 7)
+constexpr uint32_t kRingSlots = 4;            // rounds resident per lane: r-1..r (read), r+1..r+2 (landing)
+constexpr uint32_t kRingWave = kRingSlots * kRoundBytes * 64;  // 16 KiB per wave
+constexpr uint32_t kK2Slack = 3;              // K2: iterations a prefetch DMA has to land
+constexpr uint32_t kTokAhead = kK2Slack + 1;   // tokens of batch bt + 4 issued in iteration bt
+constexpr uint32_t kRecAhead = 2 * kTokAhead;  // records of batch bt + 8 issued in iteration bt
+constexpr uint32_t kTokSlots = kTokAhead;      // batches bt .. bt+3 (bt+4 reuses bt's slot)
+constexpr uint32_t kRecSlots = kTokAhead + 1;  // batches bt+4 .. bt+8
+#ifndef QLZX_K2_VMWAIT
+#define QLZX_K2_VMWAIT 6  // = 2 * kK2Slack; experiments only: other values break the prefetch invariant
+#endif
 
 __host__ __device__ inline uint32_t groups_max(uint32_t max_dsize) { return max_dsize / 31u + 2u; }
 
@@ -68,10 +74,10 @@ inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
 
 // ------------------------------------------------------------------ K1 ----
 // Ring layout per wave: [slot][piece 0..3][lane][16 B]; stream byte p of a lane
-// (q = p + shift, shift = src & 15) lives in round q/64, slot (q/64) % 3,
-// piece (q/16) % 4, byte q % 16.
+// (q = p + shift, shift = src & 15) lives in round q/64, slot (q/64) % 4,
+// piece (q/16) % 4, byte q % 16 -- i.e. at ((q/16) % 16) * 1 KiB + lane * 16 + q % 16.
 __device__ __forceinline__ uint32_t ring_off(uint32_t q, uint32_t lane) {
-    return ((((q >> 6) % kRingSlots) * 4 + ((q >> 4) & 3)) * 64 + lane) * 16 + (q & 15);
+    return (((q >> 4) & 15u) << 10) | (lane << 4) | (q & 15u);
 }
 __device__ __forceinline__ uint32_t ring_rd32(const uint8_t *ring, uint32_t q, uint32_t lane) {
     const uint32_t qa = q & ~3u;
@@ -83,14 +89,14 @@ __device__ __forceinline__ uint32_t ring_rd32(const uint8_t *ring, uint32_t q, u
 // DMA round r (q in [64r, 64r+64)) of every lane into its ring slot.  All
 // lanes always issue exactly 4 DMAs per round (inactive lanes fetch a dummy
 // chunk of the source buffer's first bytes into their own, unused, slot) so
-// that "s_waitcnt vmcnt(4)" means exactly "every round but the newest landed".
+// that "s_waitcnt vmcnt(8)" means exactly "every round but the newest two landed".
 __device__ __forceinline__ void ring_issue(uint8_t *ring_wave, const uint8_t *gbase, const uint8_t *dummy,
                                            uint32_t r, uint32_t last16, bool active) {
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {
         const uint32_t c16 = r * 4 + j;
         const uint8_t *g = (active && c16 <= last16) ? gbase + (size_t)c16 * 16 : dummy;
-        dma16(g, lds_addr(ring_wave + ((r % kRingSlots) * 4 + j) * 1024));
+        dma16(g, lds_addr(ring_wave + ((r & (kRingSlots - 1)) * 4 + j) * 1024));
     }
 }
 
@@ -156,11 +162,12 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
     const uint8_t *dummy = (const uint8_t *)(((uintptr_t)b.src) & ~(uintptr_t)15);
     ring_issue(ring, gbase, dummy, 0, last16, stream);
     ring_issue(ring, gbase, dummy, 1, last16, stream && last_round >= 1);
+    ring_issue(ring, gbase, dummy, 2, last16, stream && last_round >= 2);
     for (uint32_t r = 0;; r++) {
         if (__ballot(stream && r <= last_round) == 0) break;
-        // rounds <= r landed once at most the newest round's 4 DMAs are in flight
+        // rounds <= r landed once at most the newest two rounds' 8 DMAs are in flight
         PROF_MARK(0);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         PROF_MARK(1);  // 1: waiting for the round's DMA
         const bool act = stream && r <= last_round;
         if (CRC && act) {  // CRC of this round's bytes, in stream order
@@ -188,43 +195,38 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
             // one step = a control word (k == 31) or one item: a match token or a
             // literal run.  Straight-line selects; only the record store branches.
             const bool gb = k == 31;
-            const uint32_t bit = gb ? 0u : ((cw >> k) & 1u);
-            const uint32_t need = gb ? 4u : bit;          // bytes this step reads at ip
-            const bool end = gb ? (ip + 4 > csize) : (ip >= csize);
-            const bool wait = !end && ip + need > lim;
-            const bool stepping = go && !end && !wait;
-            const uint32_t w = ring_rd32(ring, ip + shift, lane);  // cword or token (unused for literals)
-            const uint32_t code = ((w & 3u) == 0) ? 0u : ((w & 3u) != 3u) ? 1u : ((w & 127u) != 3u) ? 2u : 3u;
-            uint32_t run = __builtin_ctz((cw >> (k & 31)) | (1u << (31 - (k & 31))));
-            if (run > csize - ip) run = csize - ip;
-            const bool rec_out = stepping && gb && g > 0;
-            const GroupRec prev{rec_ip, m, ra, rb};
-            if (rec_out) myrec[g - 1] = prev;
-            const bool sentinel_bad = stepping && gb && !(w >> 31);
-            const bool trunc_bad = stepping && bit && ip + code + 1 > csize;
-            const bool gmax_bad = stepping && gb && g >= gmax;
-            if (sentinel_bad || trunc_bad || gmax_bad) st = QLZX_E_CORRUPT;  // C1 / C2 / C5
-            const bool bad = sentinel_bad || trunc_bad || gmax_bad;
-            const bool adv = stepping && !bad;
             const uint32_t kk = k & 31;
-            if (adv) {
-                if (gb) {
-                    rec_ip = ip; cw = w; ip += 4; k = 0; m = 0; ra = 0; rb = 0; g++;
-                } else {
-                    m |= bit << kk;
-                    ra |= (bit & code) << kk;
-                    rb |= (bit & (code >> 1)) << kk;
-                    ip += bit ? code + 1 : run;
-                    k += bit ? 1u : run;
-                }
-            }
-            if (go && (end || bad)) done_parse = true;
+            const uint32_t cwk = cw >> kk;
+            const uint32_t bit = gb ? 0u : (cwk & 1u);
+            const bool end = ip + (gb ? 4u : 1u) > csize;                   // stream exhausted
+            const bool stepping = go & !end & (ip + (gb ? 4u : bit) <= lim);  // bytes read have landed
+            const uint32_t w = ring_rd32(ring, ip + shift, lane);  // cword or token (unused for literals)
+            const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
+            const uint32_t code = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);  // token bytes - 1
+            uint32_t run = __builtin_ctz(cwk | (1u << (31 - kk)));             // literal run to next match
+            run = run < csize - ip ? run : csize - ip;
+            const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) |  // C1, group bound
+                                         ((bit != 0) & (ip + code + 1 > csize)));  // C2
+            if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
+            st = bad ? QLZX_E_CORRUPT : st;
+            const bool adv = stepping & !bad;
+            const bool ag = adv & gb;
+            const uint32_t bm = bit << kk;
+            rec_ip = ag ? ip : rec_ip;
+            cw = ag ? w : cw;
+            g += ag ? 1u : 0u;
+            ip += adv ? (gb ? 4u : (bit ? code + 1 : run)) : 0u;
+            k = adv ? (gb ? 0u : k + (bit ? 1u : run)) : k;
+            m = adv ? (gb ? 0u : m | bm) : m;
+            ra = adv ? (gb ? 0u : ra | ((code & 1u) ? bm : 0u)) : ra;
+            rb = adv ? (gb ? 0u : rb | ((code & 2u) ? bm : 0u)) : rb;
+            done_parse = done_parse | (go & (end | bad));
             go = adv;
         }
         PROF_MARK(3);  // 3: parse
         if (!CRC && done_parse) stream = false;  // nothing left to read for this lane
-        // round r+2 reuses the slot of round r-2 (consumed: every lane is past 64 (r-1))
-        ring_issue(ring, gbase, dummy, r + 2, last16, stream && r + 2 <= last_round);
+        // round r+3 reuses the slot of round r-1 (consumed: round r+1 reads only rounds r, r+1)
+        ring_issue(ring, gbase, dummy, r + 3, last16, stream && r + 3 <= last_round);
     }
     PROF_MARK(4);  // 4: DMA issue + loop overhead
     if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
@@ -250,17 +252,6 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
 }
 
 // ------------------------------------------------------------------ K2 ----
-// Read 16 bytes starting at LDS byte p.
-__device__ __forceinline__ void lds_get16(const uint8_t *out, uint32_t p, uint32_t w[4]) {
-    const uint32_t *s = (const uint32_t *)(out + (p & ~3u));
-    const uint32_t pa = p & 3u;
-    const uint32_t x0 = s[0], x1 = s[1], x2 = s[2], x3 = s[3], x4 = s[4];
-    w[0] = __builtin_amdgcn_alignbyte(x1, x0, pa);
-    w[1] = __builtin_amdgcn_alignbyte(x2, x1, pa);
-    w[2] = __builtin_amdgcn_alignbyte(x3, x2, pa);
-    w[3] = __builtin_amdgcn_alignbyte(x4, x3, pa);
-}
-
 // mem = (mem & ~mask) | val in one LDS instruction (val pre-masked).
 __device__ __forceinline__ void lds_mskor(uint32_t *addr, uint32_t mask, uint32_t val) {
     const uint32_t a = (uint32_t)(uintptr_t)addr;
@@ -269,78 +260,97 @@ __device__ __forceinline__ void lds_mskor(uint32_t *addr, uint32_t mask, uint32_
 
 template <uint32_t MAXD>
 struct K2Lds {
-    uint8_t front[16];       // lets a match's first source dword start up to 4 B before out[0]
-    uint8_t out[MAXD + 32];
-    uint32_t tok[kTokSlots][64];     // per-lane token dword of batches b..b+3
-    GroupRec rec[kRecSlots][4];      // records of the <= 4 groups of batches b..b+6
+    GroupRec rec[kRecSlots][4];      // records of the <= 4 groups of batches bt+4..bt+8
+    uint32_t tok[kTokSlots][64];     // per-lane token dword of batches bt..bt+3
+    uint8_t out[MAXD + 16];          // a match's first source dword may start 4 B before out[0] (reads tok)
 };
 
 // Every K2 iteration issues exactly 2 DMA instructions (1 token dword + 1
 // record), with dummy addresses for lanes/batches past the end, so that
-// "s_waitcnt vmcnt(4)" at the end of iteration bt means "everything issued up
-// to iteration bt-2 has landed".  Iteration bt issues the tokens of bt+3 and
-// the records of bt+6, so both have two whole iterations to arrive.
-__device__ __forceinline__ void issue_rec(GroupRec (*rec)[4], const GroupRec *rb, uint32_t bt, uint32_t ngroups,
+// "s_waitcnt vmcnt(6)" at the end of iteration bt means "everything issued up
+// to iteration bt-3 has landed".  Iteration bt issues the tokens of bt+4 and
+// the records of bt+8, so both have three whole iterations to arrive.
+__device__ __forceinline__ void issue_rec(GroupRec *slot, const GroupRec *rb, uint32_t g0, uint32_t ngroups,
                                           uint32_t lane) {
-    const uint32_t g = (bt * 64) / 31 + lane;
-    if (lane < 4) dma16(g < ngroups ? (const void *)(rb + g) : (const void *)rb, lds_addr(&rec[bt % kRecSlots][0]));
+    const uint32_t g = g0 + lane;
+    if (lane < 4) dma16(g < ngroups ? (const void *)(rb + g) : (const void *)rb, lds_addr(slot));
 }
-// Item position: cword at gr.ip, then k items of which popc(a)+2popc(b) extra token bytes.
-__device__ __forceinline__ uint32_t item_pos(const GroupRec &gr, uint32_t k) {
-    const uint32_t low = (1u << k) - 1u;
-    return gr.ip + 4 + k + __builtin_popcount(gr.a & low) + 2 * __builtin_popcount(gr.b & low);
-}
-// The 4 stream bytes at min(pos, csize - 4) (unaligned dword DMA; csize >= 7
-// for a compressed level-3 stream, so the read stays inside the block).
-__device__ __forceinline__ void issue_tok(const GroupRec *recslot, uint32_t *tok, const uint8_t *src,
-                                          uint32_t csize, uint32_t bt, uint32_t nitems, uint32_t lane) {
-    const uint32_t I = bt * 64 + lane;
-    uint32_t p = 0;
-    if (I < nitems) {
-        const uint32_t g = I / 31;
-        p = item_pos(recslot[g - (bt * 64) / 31], I - g * 31);
-        p = p + 4 <= csize ? p : csize - 4;
+
+// Per-lane coordinates of item I = 64 bt + lane: group g = I / 31, index k = I % 31.
+// Advanced by one batch (64 = 2 * 31 + 2) without a division.
+struct ItemCursor {
+    uint32_t g, k;
+    __device__ __forceinline__ void next() {
+        k += 2;
+        const bool wrap = k >= 31;
+        k = wrap ? k - 31 : k;
+        g += wrap ? 3 : 2;
     }
+};
+
+// Token prefetch for one batch: returns pos | is_match << 31 for the lane's item
+// (0 past the last item) and DMAs the 4 stream bytes at min(pos, csize - 4)
+// (unaligned dword DMA; csize >= 7 for a compressed level-3 stream, so the read
+// stays inside the block).  Item position: control word at gr.ip, then k items
+// with popc(a) + 2 popc(b) extra token bytes before item k.
+__device__ __forceinline__ GroupRec tok_rec(const GroupRec *recslot, uint32_t g0, const ItemCursor &c, bool valid) {
+    return recslot[valid ? c.g - g0 : 0];
+}
+__device__ __forceinline__ uint32_t issue_tok(const GroupRec &gr, const ItemCursor &c, bool valid, uint32_t *tok,
+                                              const uint8_t *src, uint32_t csize) {
+    const uint32_t low = (1u << c.k) - 1u;
+    const uint32_t pos = gr.ip + 4 + c.k + __builtin_popcount(gr.a & low) + 2 * __builtin_popcount(gr.b & low);
+    const uint32_t p = valid ? (pos + 4 <= csize ? pos : csize - 4) : 0u;
     dma4(src + p, lds_addr(tok));
+    return valid ? (pos | (((gr.m >> c.k) & 1u) << 31)) : 0u;
 }
 
-// Byte mask of bytes [lo, hi) of one dword (lo, hi clamped to [0, 4]).
-__device__ __forceinline__ uint32_t dw_mask(int lo, int hi) {
-    lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
-    hi = hi < 0 ? 0 : (hi > 4 ? 4 : hi);
-    if (hi <= lo) return 0u;
-    const uint32_t h = hi == 4 ? 0xffffffffu : ((1u << (8 * hi)) - 1u);
-    return h & ~((1u << (8 * lo)) - 1u);
+// Branch-free level-3 token decode (quicklz.c:579-610).  Token type
+// ty = (t & 3) + ((t & 127) == 3) selects per-type bit fields from packed tables:
+//   ty 0: 1 B, off = t[2:8),  len 3          ty 1: 2 B, off = t[2:16), len 3
+//   ty 2: 2 B, off = t[6:16), len = t[2:6)+3  ty 3: 3 B, off = t[7:24), len = t[2:7)+2
+//   ty 4: 4 B, off = t[15:32), len = t[7:15)+3
+__device__ __forceinline__ void decode_tok_bf(uint32_t t, uint32_t &off, uint32_t &len, uint32_t &tl) {
+    const uint32_t ty = (t & 3u) + ((t & 127u) == 3u ? 1u : 0u);
+    const uint32_t f4 = ty * 4, f6 = ty * 6;
+    const uint32_t osh = __builtin_amdgcn_ubfe(0xF7622u, f4, 4);
+    const uint32_t ow = __builtin_amdgcn_ubfe((6u) | (14u << 6) | (10u << 12) | (17u << 18) | (17u << 24), f6, 6);
+    const uint32_t lsh = __builtin_amdgcn_ubfe(0x72200u, f4, 4);
+    const uint32_t lw = __builtin_amdgcn_ubfe(0x85400u, f4, 4);
+    const uint32_t la = __builtin_amdgcn_ubfe(0x32333u, f4, 4);
+    tl = __builtin_amdgcn_ubfe(0x43221u, f4, 4);
+    off = __builtin_amdgcn_ubfe(t, osh, ow);
+    len = __builtin_amdgcn_ubfe(t, lsh, lw) + la;
 }
 
-// One 16-byte copy step, prepared once per batch: destination dword j (at
-// qa + 4j) takes the source bytes at qa + 4j - off, i.e. alignbyte(x[j+1], x[j], sh)
-// over the aligned source dwords x[] starting at xa.
+// Byte masks of bytes [lo, lo + n) (lo < 4, n <= 16) over five dwords.
 struct Copy16 {
-    uint32_t qa, mk[5];
+    uint32_t qa, sh, mk[5];
     int xa;
-    uint32_t sh;
     __device__ __forceinline__ void prep(uint32_t q, uint32_t off, uint32_t n) {
-        qa = q & ~3u;
+        const uint32_t lo = q & 3u;
+        qa = q - lo;
         const int sa = (int)qa - (int)off;  // >= -4: out[] has a 16-B front pad
         xa = sa & ~3;
         sh = (uint32_t)sa & 3u;
-        const int lo = (int)(q & 3u), hi = lo + (int)n;
-        mk[0] = dw_mask(lo, hi);
-        mk[1] = dw_mask(lo - 4, hi - 4);
-        mk[2] = dw_mask(lo - 8, hi - 8);
-        mk[3] = dw_mask(lo - 12, hi - 12);
-        mk[4] = dw_mask(lo - 16, hi - 16);
+        const int H = 8 * (int)(lo + n);
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            int sj = 32 * (j + 1) - H;
+            sj = sj < 0 ? 0 : (sj > 32 ? 32 : sj);
+            mk[j] = (uint32_t)(0xffffffffull >> sj);
+        }
+        mk[0] &= 0xffffffffu << (8 * lo);
     }
     __device__ __forceinline__ void run(uint8_t *out) const {
         const uint32_t *x = (const uint32_t *)(out + xa);
         const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4], x5 = x[5];
         uint32_t *dw = (uint32_t *)(out + qa);
-        if (mk[0]) lds_mskor(dw + 0, mk[0], __builtin_amdgcn_alignbyte(x1, x0, sh) & mk[0]);
-        if (mk[1]) lds_mskor(dw + 1, mk[1], __builtin_amdgcn_alignbyte(x2, x1, sh) & mk[1]);
-        if (mk[2]) lds_mskor(dw + 2, mk[2], __builtin_amdgcn_alignbyte(x3, x2, sh) & mk[2]);
-        if (mk[3]) lds_mskor(dw + 3, mk[3], __builtin_amdgcn_alignbyte(x4, x3, sh) & mk[3]);
-        if (mk[4]) lds_mskor(dw + 4, mk[4], __builtin_amdgcn_alignbyte(x5, x4, sh) & mk[4]);
+        lds_mskor(dw + 0, mk[0], __builtin_amdgcn_alignbyte(x1, x0, sh) & mk[0]);
+        lds_mskor(dw + 1, mk[1], __builtin_amdgcn_alignbyte(x2, x1, sh) & mk[1]);
+        lds_mskor(dw + 2, mk[2], __builtin_amdgcn_alignbyte(x3, x2, sh) & mk[2]);
+        lds_mskor(dw + 3, mk[3], __builtin_amdgcn_alignbyte(x4, x3, sh) & mk[3]);
+        lds_mskor(dw + 4, mk[4], __builtin_amdgcn_alignbyte(x5, x4, sh) & mk[4]);
     }
 };
 
@@ -353,6 +363,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return v;
+}
+
+__device__ __forceinline__ uint32_t ff1_or(uint64_t m, uint32_t dflt) {
+    return m ? (uint32_t)__builtin_ctzll(m) : dflt;
 }
 
 template <uint32_t MAXD>
@@ -382,103 +396,120 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
     const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
     const uint32_t nb = (nitems + 63) / 64;
     const uint32_t tail_from = dsize > QLZX_TAIL ? dsize - 1 - QLZX_TAIL : 0;  // op >= this: tail (quicklz.c:503)
-    // prologue: records of batches 0..5, then the tokens of batches 0..2
-    for (uint32_t j = 0; j < 6; j++) issue_rec(L.rec, rb, j, ngroups, lane);
+
+    // prologue: records of batches 0..3, the tokens of batches 0..3 (which read
+    // those records), then the records of batches 4..7 (slots 4, 0, 1, 2)
+    for (uint32_t j = 0; j < kTokAhead; j++) issue_rec(L.rec[j], rb, (j * 64) / 31, ngroups, lane);
     vm_sync();
-    for (uint32_t j = 0; j < 3; j++) issue_tok(L.rec[j], L.tok[j], src, csize, j, nitems, lane);
+    ItemCursor cur{lane / 31, lane % 31};  // item coordinates of the next batch to issue
+    uint32_t pm[kTokAhead];
+#pragma unroll
+    for (uint32_t j = 0; j < kTokAhead; j++) {
+        const bool v = j * 64 + lane < nitems;
+        pm[j] = issue_tok(tok_rec(L.rec[j], (j * 64) / 31, cur, v), cur, v, L.tok[j], src, csize);
+        cur.next();
+    }
+    for (uint32_t j = kTokAhead; j < kRecAhead; j++) issue_rec(L.rec[j % kRecSlots], rb, (j * 64) / 31, ngroups, lane);
     vm_sync();
     PROF_DECL
-    uint32_t D = 0;
-    bool bad = false, tail = false, complete = dsize == 0;
-    for (uint32_t bt = 0; bt < nb && !complete && !bad; bt++) {
-        // invariant: tok[bt..bt+2] and rec[bt..bt+5] landed.  Read this batch's state first.
-        const uint32_t I = bt * 64 + lane;
-        const bool valid = I < nitems;
-        const uint32_t g = I / 31;
-        const GroupRec gr = L.rec[bt % kRecSlots][valid ? g - (bt * 64) / 31 : 0];
-        const uint32_t tw = L.tok[bt % kTokSlots][lane];
+    uint32_t D = 0;                   // output bytes of all earlier batches
+    bool err = false;                 // per-lane: a check failed on this lane's item
+    bool tail = false, complete = dsize == 0;
+    // slot counters: tokens of bt (read) and bt+4 (issue); records of bt+4 (read) and bt+8 (issue)
+    uint32_t ts = 0, rs4 = kTokAhead % kRecSlots, rs8 = kRecAhead % kRecSlots;
+    for (uint32_t bt = 0; bt < nb && !complete; bt++) {
+        // this batch's token dword, and the record the prefetch of batch bt+4 needs;
+        // both reads complete before that prefetch reuses this batch's token slot
+        const uint32_t tw = L.tok[ts][lane];
+        const bool v4 = (bt + kTokAhead) * 64 + lane < nitems;
+        const GroupRec gr4 = tok_rec(L.rec[rs4], ((bt + kTokAhead) * 64) / 31, cur, v4);
         lds_sync();
-        PROF_MARK(0);  // 0: batch state reads
-        // prefetch: tokens of bt+3 (its records landed), records of bt+6
-        issue_tok(L.rec[(bt + 3) % kRecSlots], L.tok[(bt + 3) % kTokSlots], src, csize, bt + 3, nitems, lane);
-        issue_rec(L.rec, rb, bt + 6, ngroups, lane);
+        const uint32_t posm = pm[0];
+#pragma unroll
+        for (uint32_t j = 0; j + 1 < kTokAhead; j++) pm[j] = pm[j + 1];
+        pm[kTokAhead - 1] = issue_tok(gr4, cur, v4, L.tok[ts], src, csize);
+        cur.next();
+        issue_rec(L.rec[rs8], rb, ((bt + kRecAhead) * 64) / 31, ngroups, lane);
+        ts = ts == kTokSlots - 1 ? 0 : ts + 1;
+        rs4 = rs4 == kRecSlots - 1 ? 0 : rs4 + 1;
+        rs8 = rs8 == kRecSlots - 1 ? 0 : rs8 + 1;
         PROF_MARK(1);  // 1: prefetch issue
-        const uint32_t k = I - g * 31;
-        const bool is_match = valid && ((gr.m >> k) & 1u);
-        const uint32_t pos = item_pos(gr, k);
+        const bool valid = bt * 64 + lane < nitems;
+        const bool ism = (posm >> 31) != 0;
+        const uint32_t pos = posm & 0x7fffffffu;
         const uint32_t t = pos + 4 <= csize ? tw : tw >> (8 * (pos + 4 - csize));
-        uint32_t off = 0, len = valid ? 1u : 0u, tl = 1;
-        if (is_match) tl = decode_token(t, off, len);
+        uint32_t off, mlen, tl;
+        decode_tok_bf(t, off, mlen, tl);
+        const uint32_t len = ism ? mlen : (valid ? 1u : 0u);
+        tl = ism ? tl : 1u;
         const uint32_t incl = wave_incl_scan(len);
         const uint32_t d = D + incl - len;
-        const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+        D += __builtin_amdgcn_readlane(incl, 63);
         // ---- checks C2-C5 on the live items (those that start before dsize) ----
         const bool live = valid && d < dsize;
-        const uint64_t tail_lanes = __ballot(live && !is_match && d >= tail_from);
-        const uint32_t tail_lane = tail ? 0u : (tail_lanes ? (uint32_t)__builtin_ctzll(tail_lanes) : 64u);  // C4
-        bool ok = true;
-        if (live && is_match)  // C3, and C4: no match after the first tail literal
-            ok = off >= 3 && off <= d && d + len + 4 <= dsize && lane < tail_lane;
-        if (live && d + len == dsize) {  // the item that completes dsize: C5
-            const uint32_t ip_end = pos + tl;
-            ok = ok && (ip_end == csize || (ip_end < hdr + 9 && csize == hdr + 9));
-        }
-        if (__ballot(live && !ok)) { bad = true; break; }
+        const uint64_t tail_lanes = __ballot(live && !ism && d >= tail_from);
+        const uint32_t tail_lane = tail ? 0u : ff1_or(tail_lanes, 64u);  // C4: no match after it
         tail = tail || tail_lanes != 0;
-        complete = __ballot(live && d + len == dsize) != 0;
+        const bool mok = off >= 3 && off <= d && d + len + 4 <= dsize && lane < tail_lane;  // C3, C4
+        const bool last = live && d + len == dsize;  // C5: the item completing dsize ends the stream
+        const uint32_t ip_end = pos + tl;
+        const bool eok = ip_end == csize || (ip_end < hdr + 9 && csize == hdr + 9);
+        const bool bad = live && ((ism && !mok) || (last && !eok));
+        err = err || bad;
+        complete = __ballot(last) != 0;
         PROF_MARK(2);  // 2: decode + scan + checks
-        if (live && !is_match) out[d] = (uint8_t)t;
+        // literals (non-literal lanes store to an unused byte past MAXD)
+        out[(live && !ism) ? d : MAXD + 8] = (uint8_t)t;
         // ---- matches: copy in sub-rounds ----
-        const bool mlive = live && is_match;
-        bool done = !mlive;
+        bool done = !(live && ism && !bad);
         const uint32_t s = d - off;
         const uint32_t send = (s + len < d) ? s + len : d;
         const uint32_t end = d + len;
-        const bool bytewise = off < 16 && off < len;
+        const bool spec = off < len || len > 16;  // overlapping or long: byte / chunked path
         Copy16 cp;
         cp.prep(d, off, len < 16 ? len : 16);
-        for (;;) {
-            lds_sync();
-            uint64_t pend = __ballot(!done);
-            if (!pend) break;
+        uint64_t pend = __ballot(!done);
+        while (pend) {
             // the first three pending matches bound three gaps whose bytes are all final
             const uint32_t u0 = (uint32_t)__builtin_ctzll(pend);
-            pend &= pend - 1;
-            const uint32_t u1 = pend ? (uint32_t)__builtin_ctzll(pend) : u0;
-            pend &= pend - 1;
-            const uint32_t u2 = pend ? (uint32_t)__builtin_ctzll(pend) : u1;
+            const uint64_t p1 = pend & (pend - 1), p2 = p1 & (p1 - 1);
+            const uint32_t u1 = ff1_or(p1, u0), u2 = ff1_or(p2, u0);
             const uint32_t d0 = __builtin_amdgcn_readlane(d, u0), e0 = __builtin_amdgcn_readlane(end, u0);
-            const uint32_t d1 = u1 != u0 ? __builtin_amdgcn_readlane(d, u1) : 0xffffffffu;
-            const uint32_t e1 = __builtin_amdgcn_readlane(end, u1);
-            const uint32_t d2 = u2 != u1 ? __builtin_amdgcn_readlane(d, u2) : 0xffffffffu;
-            const bool ready = !done && (send <= d0 || (s >= e0 && send <= d1) || (u1 != u0 && s >= e1 && send <= d2));
-            if (ready) {
-                if (bytewise) {
-                    uint32_t j2 = 0;
-                    for (uint32_t j = 0; j < len; j++) {
-                        out[d + j] = out[s + j2];
-                        j2 = (j2 + 1 == off) ? 0 : j2 + 1;
-                    }
-                } else {
-                    cp.run(out);
-                    for (uint32_t c = 16; c < len; c += 16) {  // long matches, chunk by chunk
-                        if (off < len) lds_sync();
-                        Copy16 c2;
-                        c2.prep(d + c, off, len - c < 16 ? len - c : 16);
-                        c2.run(out);
+            const uint32_t d1r = __builtin_amdgcn_readlane(d, u1), e1 = __builtin_amdgcn_readlane(end, u1);
+            const uint32_t d2r = __builtin_amdgcn_readlane(d, u2);
+            const uint32_t d1 = p1 ? d1r : 0xffffffffu, d2 = p2 ? d2r : 0xffffffffu;
+            const bool ready = !done & ((send <= d0) | ((s >= e0) & (send <= d1)) | ((s >= e1) & (send <= d2)));
+            if (ready && !spec) cp.run(out);
+            if (__ballot(ready && spec)) {
+                if (ready && spec) {
+                    if (off < 16 && off < len) {  // short-period overlap: byte by byte
+                        uint32_t j2 = 0;
+                        for (uint32_t j = 0; j < len; j++) {
+                            out[d + j] = out[s + j2];
+                            j2 = (j2 + 1 == off) ? 0 : j2 + 1;
+                        }
+                    } else {  // 16-B chunks, in order when the source overlaps the destination
+                        for (uint32_t c = 0; c < len; c += 16) {
+                            if (c && off < len) lds_sync();
+                            Copy16 c2;
+                            c2.prep(d + c, off, len - c < 16 ? len - c : 16);
+                            c2.run(out);
+                        }
                     }
                 }
-                done = true;
             }
+            done = done || ready;
+            lds_sync();
+            pend = __ballot(!done);
         }
         PROF_MARK(3);  // 3: match sub-rounds
-        D += total;
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // DMAs of iterations <= bt-1 landed
+        if (__ballot(err)) break;
+        asm volatile("s_waitcnt vmcnt(" QLZX_STR(QLZX_K2_VMWAIT) ")" ::: "memory");  // DMAs of iterations <= bt-3 landed
         PROF_MARK(4);  // 4: waiting for prefetch
     }
     vm_sync();
     lds_sync();
-    if (bad || !complete) {
+    if (__ballot(err) || !complete) {
         if (lane == 0) { status[i] = QLZX_E_CORRUPT; if (dsize_out) dsize_out[i] = 0; }
         return;
     }

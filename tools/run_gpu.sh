@@ -2,5 +2,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 120 rocprofv3 -L > gpurun_out/ctrs.txt 2>&1
-bash tools/pmc.sh pmc1 "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM SQ_BUSY_CYCLES" "FETCH_SIZE" "WRITE_SIZE"
+timeout -k 10 300 python -m pytest tests -x -q -m gpu > gpurun_out/r9_pytest.txt 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/r9_pytest.txt; exit 1; }
+tail -2 gpurun_out/r9_pytest.txt
+QLZX_LIB=gobeansdb_amd/libqlzx_prof.so timeout -k 10 200 python tools/phase_prof.py > gpurun_out/ph8.txt 2>&1 && cat gpurun_out/ph8.txt
+bash tools/prof.sh p8 --blocks 262144 --steps 3 --warmup 1 --cpu-seconds 0 | grep "k_dec"
