@@ -49,7 +49,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--crc", action="store_true", help="fused record CRC verify in the timed pass")
-    p.add_argument("--traffic-json", default=None, help="PMC HBM bytes per launch (profiles/*.json)")
+    p.add_argument("--traffic-json", default=None,
+                   help="PMC HBM bytes per block (tools/traffic.py output); default: the committed "
+                        "profiles/r01_c2_traffic.json for the c2 workload")
     return p.parse_args()
 
 
@@ -154,8 +156,12 @@ def main():
     value = total_out / wall / 2**30
     achieved = (csum + dsum) / (kern_ms * 1e-3) / 1e9
     traffic = None
+    if args.traffic_json is None and args.mode == "decompress" and kind == "text" and bs == 16384 and not args.crc:
+        args.traffic_json = os.path.join(ROOT, "profiles", "r01_c2_traffic.json")
     if args.traffic_json and os.path.exists(args.traffic_json):
-        traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+        # PMC-measured HBM bytes per block (tools/traffic.py) x blocks per launch
+        tj = json.load(open(args.traffic_json))
+        traffic = round(tj["hbm_bytes_per_block"] * n)
 
     cpu = None
     if rank == 0 and not args.no_cpu:
