@@ -57,11 +57,9 @@ def parse():
 
 def main():
     args = parse()
-    from gobeansdb_amd import _lib, batch
+    from gobeansdb_amd import _lib, batch, shard
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = shard.env_rank()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -80,7 +78,7 @@ def main():
     cbuf = torch.empty(ctotal, dtype=torch.uint8, device=dev)
     coff_t = torch.from_numpy(coff.view(np.int64)).to(dev)
     cs_parts = []
-    first = rank * n
+    first, _ = shard.weak_shard(rank, n)   # weak scaling: each rank owns its own block ids
     for c0 in range(0, uniq, args.gen_chunk):
         m = min(args.gen_chunk, uniq - c0)
         plain = batch.synth(kind, 0x5EED2026, [bs] * m, first_id=first + c0, device=dev)
@@ -146,13 +144,11 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t_start
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
-    if world > 1:
-        tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        wall, kern_ms = float(tt[0]), float(tt[1])
+    wall, kern_ms = shard.max_over_ranks([wall, kern_ms], device=dev)   # the slowest rank counts
+    tot = shard.sum_over_ranks({"out_bytes": dsum, "in_bytes": csum}, device=dev)
     ms_per_step = wall * 1e3 / args.steps
 
-    total_out = dsum * world * args.steps
+    total_out = tot["out_bytes"] * args.steps
     value = total_out / wall / 2**30
     achieved = (csum + dsum) / (kern_ms * 1e-3) / 1e9
     traffic = None
