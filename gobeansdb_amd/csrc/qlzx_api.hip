@@ -16,6 +16,7 @@
 #include "qlzx_encode_lane.hip"
 #include "qlzx_encode_wg.hip"
 #include "qlzx_crc.hip"
+#include "qlzx_replay.hip"
 
 namespace {
 
@@ -176,6 +177,33 @@ int qlzx_synth_batch(int kind, uint64_t seed, uint64_t first_id, uint8_t *dst, c
         return fail(QLZX_R_BAD_ARG, "qlzx_synth_batch: null arg");
     hipLaunchKernelGGL(qlzx::k_synth, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, kind, seed,
                        first_id, dst, dst_off, len, n, vocab, vocab_off, zipf_cdf, nwords);
+    HIP_OK(hipGetLastError());
+    return QLZX_R_OK;
+}
+
+size_t qlzx_replay_workspace_size(uint64_t size) { return qlzx::replay_ws_layout(size, nullptr, nullptr); }
+
+int qlzx_replay_index(const uint8_t *data, uint64_t size, uint64_t start, uint32_t max_key, uint64_t body_max,
+                      uint64_t *rec_off, uint32_t *rec_broken, uint32_t *result, void *workspace,
+                      size_t workspace_bytes, void *stream) {
+    if ((!data && size) || !rec_off || !rec_broken || !result)
+        return fail(QLZX_R_BAD_ARG, "qlzx_replay_index: null arg");
+    if (start % 256 != 0 || start > size) return fail(QLZX_R_BAD_ARG, "qlzx_replay_index: start not a slot");
+    if (size / 256 >= 0xfffffff0ull) return fail(QLZX_R_BAD_ARG, "qlzx_replay_index: file too large");
+    if (!workspace || workspace_bytes < qlzx_replay_workspace_size(size))
+        return fail(QLZX_R_WORKSPACE, "qlzx_replay_index: workspace too small");
+    const int e = qlzx::launch_replay_index(data, size, start, max_key, body_max, rec_off, rec_broken, result,
+                                            workspace, (hipStream_t)stream);
+    if (e) return fail(QLZX_R_HIP, "qlzx_replay_index", (hipError_t)e);
+    return QLZX_R_OK;
+}
+
+int qlzx_vhash_batch(const uint8_t *src, const uint64_t *off, const uint32_t *len, uint32_t n, uint16_t *out,
+                     void *stream) {
+    if (n == 0) return QLZX_R_OK;
+    if (!src || !off || !len || !out) return fail(QLZX_R_BAD_ARG, "qlzx_vhash_batch: null arg");
+    hipLaunchKernelGGL(qlzx::k_vhash, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, src, off, len, n,
+                       out);
     HIP_OK(hipGetLastError());
     return QLZX_R_OK;
 }

@@ -270,10 +270,11 @@ struct K2Lds {
 // "s_waitcnt vmcnt(6)" at the end of iteration bt means "everything issued up
 // to iteration bt-3 has landed".  Iteration bt issues the tokens of bt+4 and
 // the records of bt+8, so both have three whole iterations to arrive.
+template <bool DMA = true>
 __device__ __forceinline__ void issue_rec(GroupRec *slot, const GroupRec *rb, uint32_t g0, uint32_t ngroups,
                                           uint32_t lane) {
     const uint32_t g = g0 + lane;
-    if (lane < 4) dma16(g < ngroups ? (const void *)(rb + g) : (const void *)rb, lds_addr(slot));
+    if (DMA && lane < 4) dma16(g < ngroups ? (const void *)(rb + g) : (const void *)rb, lds_addr(slot));
 }
 
 // Per-lane coordinates of item I = 64 bt + lane: group g = I / 31, index k = I % 31.
@@ -296,12 +297,14 @@ struct ItemCursor {
 __device__ __forceinline__ GroupRec tok_rec(const GroupRec *recslot, uint32_t g0, const ItemCursor &c, bool valid) {
     return recslot[valid ? c.g - g0 : 0];
 }
+template <bool DMA = true>
 __device__ __forceinline__ uint32_t issue_tok(const GroupRec &gr, const ItemCursor &c, bool valid, uint32_t *tok,
-                                              const uint8_t *src, uint32_t csize) {
+                                              const uint8_t *src, uint32_t csize, uint32_t *pout = nullptr) {
     const uint32_t low = (1u << c.k) - 1u;
     const uint32_t pos = gr.ip + 4 + c.k + __builtin_popcount(gr.a & low) + 2 * __builtin_popcount(gr.b & low);
     const uint32_t p = valid ? (pos + 4 <= csize ? pos : csize - 4) : 0u;
-    dma4(src + p, lds_addr(tok));
+    if (DMA) dma4(src + p, lds_addr(tok));
+    if (pout) *pout = p;
     return valid ? (pos | (((gr.m >> c.k) & 1u) << 31)) : 0u;
 }
 
@@ -403,10 +406,19 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
     vm_sync();
     ItemCursor cur{lane / 31, lane % 31};  // item coordinates of the next batch to issue
     uint32_t pm[kTokAhead];
+#ifdef QLZX_K2_REGTOK
+    uint32_t twr[kTokAhead];
+#endif
 #pragma unroll
     for (uint32_t j = 0; j < kTokAhead; j++) {
         const bool v = j * 64 + lane < nitems;
+#ifdef QLZX_K2_REGTOK
+        uint32_t pj;
+        pm[j] = issue_tok<false>(tok_rec(L.rec[j], (j * 64) / 31, cur, v), cur, v, L.tok[j], src, csize, &pj);
+        twr[j] = *(const uint32_t *)(src + pj);
+#else
         pm[j] = issue_tok(tok_rec(L.rec[j], (j * 64) / 31, cur, v), cur, v, L.tok[j], src, csize);
+#endif
         cur.next();
     }
     for (uint32_t j = kTokAhead; j < kRecAhead; j++) issue_rec(L.rec[j % kRecSlots], rb, (j * 64) / 31, ngroups, lane);
@@ -420,16 +432,35 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
     for (uint32_t bt = 0; bt < nb && !complete; bt++) {
         // this batch's token dword, and the record the prefetch of batch bt+4 needs;
         // both reads complete before that prefetch reuses this batch's token slot
+#ifdef QLZX_K2_REGTOK
+        const uint32_t tw = twr[0];
+#pragma unroll
+        for (uint32_t j = 0; j + 1 < kTokAhead; j++) twr[j] = twr[j + 1];
+#else
         const uint32_t tw = L.tok[ts][lane];
+#endif
         const bool v4 = (bt + kTokAhead) * 64 + lane < nitems;
         const GroupRec gr4 = tok_rec(L.rec[rs4], ((bt + kTokAhead) * 64) / 31, cur, v4);
         lds_sync();
         const uint32_t posm = pm[0];
 #pragma unroll
         for (uint32_t j = 0; j + 1 < kTokAhead; j++) pm[j] = pm[j + 1];
-        pm[kTokAhead - 1] = issue_tok(gr4, cur, v4, L.tok[ts], src, csize);
+#ifdef QLZX_EXP_NODMA  // experiment: no loop prefetch (wrong output; timing only)
+        constexpr bool kLoopDma = false;
+#else
+        constexpr bool kLoopDma = true;
+#endif
+#ifdef QLZX_K2_REGTOK
+        {
+            uint32_t p4;
+            pm[kTokAhead - 1] = issue_tok<false>(gr4, cur, v4, L.tok[ts], src, csize, &p4);
+            twr[kTokAhead - 1] = *(const uint32_t *)(src + p4);
+        }
+#else
+        pm[kTokAhead - 1] = issue_tok<kLoopDma>(gr4, cur, v4, L.tok[ts], src, csize);
+#endif
         cur.next();
-        issue_rec(L.rec[rs8], rb, ((bt + kRecAhead) * 64) / 31, ngroups, lane);
+        issue_rec<kLoopDma>(L.rec[rs8], rb, ((bt + kRecAhead) * 64) / 31, ngroups, lane);
         ts = ts == kTokSlots - 1 ? 0 : ts + 1;
         rs4 = rs4 == kRecSlots - 1 ? 0 : rs4 + 1;
         rs8 = rs8 == kRecSlots - 1 ? 0 : rs8 + 1;
@@ -479,7 +510,9 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
             const uint32_t d2r = __builtin_amdgcn_readlane(d, u2);
             const uint32_t d1 = p1 ? d1r : 0xffffffffu, d2 = p2 ? d2r : 0xffffffffu;
             const bool ready = !done & ((send <= d0) | ((s >= e0) & (send <= d1)) | ((s >= e1) & (send <= d2)));
+#ifndef QLZX_EXP_NOCOPY
             if (ready && !spec) cp.run(out);
+#endif
             if (__ballot(ready && spec)) {
                 if (ready && spec) {
                     if (off < 16 && off < len) {  // short-period overlap: byte by byte
@@ -503,12 +536,15 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
             pend = __ballot(!done);
         }
         PROF_MARK(3);  // 3: match sub-rounds
+#ifndef QLZX_EXP_NOBREAK
         if (__ballot(err)) break;
+#endif
         asm volatile("s_waitcnt vmcnt(" QLZX_STR(QLZX_K2_VMWAIT) ")" ::: "memory");  // DMAs of iterations <= bt-3 landed
         PROF_MARK(4);  // 4: waiting for prefetch
     }
     vm_sync();
     lds_sync();
+    PROF_FLUSH(1);
     if (__ballot(err) || !complete) {
         if (lane == 0) { status[i] = QLZX_E_CORRUPT; if (dsize_out) dsize_out[i] = 0; }
         return;
@@ -523,8 +559,7 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
             for (uint32_t q = p; q < e; q++) dst[q] = out[q];
         }
     }
-    PROF_MARK(5);  // 5: write-out
-    PROF_FLUSH(1);
+    PROF_MARK(5);  // 5: write-out (not flushed: stamps of the loop only)
     if (lane == 0) {
         status[i] = QLZX_OK;
         if (dsize_out) dsize_out[i] = dsize;

@@ -1,0 +1,345 @@
+// qlzx_replay.hip -- batched replay of a .data chunk:
+// record discovery with the nextValid resync of DataStreamReader
+// (store/datafile.go:202-277), record CRC verify (store/datafile.go:66-76,
+// 161-168) and the value hash Getvhash/Fnv1a (store/item.go:89-100,
+// utils/hash.go:8-16).
+//
+// The sequential reader becomes data-parallel in four steps:
+//   1. every 256-B slot is classified from its 24-B header (k_rp_slots); the
+//      plausible ones (1 <= ksz <= max_key, vsz <= body_max, fits the file)
+//      become candidates;
+//   2. one wave per candidate computes the record CRC (k_rp_crc): rsz[s] = the
+//      padded record size when readRecordAt(256 s) would succeed, else 0;
+//   3. valid slots are compacted in order (A[]), and each gets its successor:
+//      the reader, at the end p of record A[i], either hits an error (partial
+//      header / truncated record with valid sizes: Next() returns an error),
+//      reads the record at p (valid) or resyncs to the first valid slot >= p
+//      (nextValid).  Because vidx[] is the exclusive count of valid slots,
+//      "first valid slot >= p" is simply index vidx[p / 256];
+//   4. the path from the start position is marked by pointer doubling
+//      (log2 rounds) and compacted into the visited record list with each
+//      record's sizeBroken.
+#include "qlzx_device.h"
+
+namespace qlzx {
+
+constexpr uint32_t kRpSlot = 256;
+constexpr uint32_t kRpHdr = 24;
+enum : uint8_t { kSlotBadSize = 1, kSlotTrunc = 2, kSlotPartial = 3, kSlotCand = 4 };
+constexpr uint32_t kScanTile = 1024;  // elements per scan tile (256 threads x 4)
+
+struct RpCounters {
+    uint32_t ncand, m, r0, nvis, end_kind, pad[3];
+};
+
+__device__ __forceinline__ uint32_t ld32u(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// 1. slot classification (readRecordAt's size checks, store/datafile.go:128-136)
+__global__ void __launch_bounds__(256) k_rp_slots(const uint8_t *data, uint64_t size, uint32_t nslots,
+                                                  uint32_t max_key, uint64_t body_max, uint8_t *kind,
+                                                  uint32_t *rsz, uint32_t *cand, RpCounters *cnt) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nslots) return;
+    const uint64_t off = (uint64_t)s * kRpSlot;
+    rsz[s] = 0;
+    uint8_t k;
+    if (off + kRpHdr > size) {
+        k = kSlotPartial;
+    } else {
+        const uint8_t *h = data + off;
+        const uint32_t ksz = ld32u(h + 16), vsz = ld32u(h + 20);
+        if (ksz == 0 || ksz > max_key || (uint64_t)vsz > body_max) k = kSlotBadSize;
+        else if (off + kRpHdr + ksz + vsz > size) k = kSlotTrunc;
+        else k = kSlotCand;
+    }
+    kind[s] = k;
+    if (k == kSlotCand) cand[atomicAdd(&cnt->ncand, 1u)] = s;
+}
+
+// 2. record CRC of every candidate, one wave each (wave_crc_raw of qlzx_crc.hip)
+__device__ uint32_t wave_crc_raw(const uint32_t *tab, const uint8_t *p, uint64_t len, uint32_t lane);
+
+__global__ void __launch_bounds__(256) k_rp_crc(const uint8_t *data, const uint32_t *cand,
+                                                const RpCounters *cnt, uint32_t *rsz) {
+    __shared__ uint32_t tab[256];
+    load_crc_table(tab);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nc = cnt->ncand;
+    for (uint32_t c = blockIdx.x * 4 + threadIdx.x / 64; c < nc; c += gridDim.x * 4) {
+        const uint32_t s = cand[c];
+        const uint8_t *h = data + (uint64_t)s * kRpSlot;
+        const uint32_t ksz = ld32u(h + 16), vsz = ld32u(h + 20);
+        const uint32_t len = 20 + ksz + vsz;  // header[4:24] ‖ key ‖ value
+        const uint32_t raw = wave_crc_raw(tab, h + 4, len, lane);
+        const uint32_t crc = (raw ^ crc_shift(0xffffffffu, len)) ^ 0xffffffffu;
+        if (lane == 0 && crc == ld32u(h)) rsz[s] = ((kRpHdr + ksz + vsz + 255u) >> 8) << 8;
+    }
+}
+
+// ---- exclusive scan of per-element 0/1 flags over [0, n), three kernels ----
+struct ValidFlag {  // slot s is a valid record start
+    const uint32_t *rsz;
+    __device__ uint32_t operator()(uint32_t i) const { return rsz[i] != 0; }
+};
+struct VisitFlag {  // valid index i < m lies on the reader's path (m, m+1 are the end markers)
+    const uint8_t *flag;
+    const RpCounters *cnt;
+    __device__ uint32_t operator()(uint32_t i) const { return i < cnt->m ? flag[i] : 0u; }
+};
+
+template <class F>
+__global__ void __launch_bounds__(256) k_scan_tiles(F f, uint32_t n, uint32_t *tile_sum) {
+    __shared__ uint32_t part[4];
+    const uint32_t base = blockIdx.x * kScanTile;
+    uint32_t c = 0;
+    for (uint32_t j = threadIdx.x; j < kScanTile; j += 256)
+        if (base + j < n) c += f(base + j);
+    for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tile_sum[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// single workgroup: exclusive scan of tile sums in place; *total = sum
+__global__ void __launch_bounds__(1024) k_scan_top(uint32_t *tile_sum, uint32_t ntiles, uint32_t *total) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t base = 0; base < ntiles; base += 1024) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < ntiles ? tile_sum[i] : 0u;
+        uint32_t x = v;  // inclusive wave scan
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= (uint32_t)d) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int j = 0; j < 16; j++) { const uint32_t t = wsum[j]; wsum[j] = acc; acc += t; }
+        }
+        __syncthreads();
+        const uint32_t excl = carry + wsum[w] + x - v;
+        if (i < ntiles) tile_sum[i] = excl;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = excl + v;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+// per tile: local exclusive ranks + the tile's offset; g(i, idx, flag) scatters
+template <class F, class G>
+__global__ void __launch_bounds__(256) k_scan_apply(F f, G g, uint32_t n, const uint32_t *tile_sum) {
+    __shared__ uint32_t wsum[4];
+    const uint32_t base = blockIdx.x * kScanTile + threadIdx.x * 4;
+    uint32_t v[4], c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        v[j] = (base + j < n) ? f(base + j) : 0u;
+        c += v[j];
+    }
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = c;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t woff = 0;
+    for (uint32_t j = 0; j < w; j++) woff += wsum[j];
+    uint32_t idx = tile_sum[blockIdx.x] + woff + x - c;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        if (base + j < n) g(base + j, idx, v[j]);
+        idx += v[j];
+    }
+}
+
+struct ScatterValid {  // vidx[s] = #valid slots before s; A[vidx] = s for valid s
+    uint32_t *vidx, *A;
+    __device__ void operator()(uint32_t s, uint32_t idx, uint32_t v) const {
+        vidx[s] = idx;
+        if (v) A[idx] = s;
+    }
+};
+struct ScatterVisit {  // visited valid index i -> output position
+    const uint32_t *A;
+    uint32_t *vis;
+    __device__ void operator()(uint32_t i, uint32_t idx, uint32_t v) const {
+        if (v) vis[idx] = A[i];
+    }
+};
+
+// Where the reader goes from byte position p (256-aligned): the index of the
+// record it returns next (m = clean end, m + 1 = error).  Next() semantics,
+// store/datafile.go:228-277.
+__device__ __forceinline__ uint32_t rp_step(uint64_t p, uint64_t size, uint32_t nslots, const uint8_t *kind,
+                                            const uint32_t *vidx, uint32_t m) {
+    if (p >= size) return m;                           // io.EOF: err = nil, no record
+    const uint32_t sp = (uint32_t)(p / kRpSlot);
+    const uint8_t k = kind[sp];
+    if (k == kSlotPartial || k == kSlotTrunc) return m + 1;  // io.ReadFull: unexpected EOF
+    return sp < nslots ? vidx[sp] : m;                 // valid here, or nextValid's first valid slot >= p
+}
+
+__global__ void __launch_bounds__(256) k_rp_next(uint64_t size, uint32_t nslots, uint64_t start,
+                                                 const uint8_t *kind, const uint32_t *rsz, const uint32_t *vidx,
+                                                 const uint32_t *A, RpCounters *cnt, uint32_t *nxt, uint8_t *flag) {
+    const uint32_t m = cnt->m;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) {
+        const uint32_t s = A[i];
+        nxt[i] = rp_step((uint64_t)s * kRpSlot + rsz[s], size, nslots, kind, vidx, m);
+        flag[i] = 0;
+    } else if (i == m || i == m + 1) {
+        nxt[i] = i;  // absorbing end / error
+        flag[i] = 0;
+    }
+    if (i == 0) cnt->r0 = rp_step(start, size, nslots, kind, vidx, m);
+}
+
+__global__ void __launch_bounds__(256) k_rp_seed(RpCounters *cnt, uint8_t *flag) { flag[cnt->r0] = 1; }
+
+// one pointer-doubling round: flag J(i) for flagged i; J2 = J o J
+__global__ void __launch_bounds__(256) k_rp_double(const RpCounters *cnt, const uint32_t *J, uint32_t *J2,
+                                                   uint8_t *flag) {
+    const uint32_t m = cnt->m;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m + 2) return;
+    const uint32_t j = J[i];
+    if (flag[i]) flag[j] = 1;
+    J2[i] = J[j];
+}
+
+__global__ void __launch_bounds__(256) k_rp_emit(const uint32_t *vis, const RpCounters *cnt, const uint32_t *rsz,
+                                                 uint64_t start, uint64_t *rec_off, uint32_t *rec_broken) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= cnt->nvis) return;
+    const uint64_t off = (uint64_t)vis[k] * kRpSlot;
+    const uint64_t prev_end = k == 0 ? start : (uint64_t)vis[k - 1] * kRpSlot + rsz[vis[k - 1]];
+    rec_off[k] = off;
+    rec_broken[k] = (uint32_t)(off - prev_end);  // sizeBroken: bytes nextValid skipped
+}
+
+__global__ void k_rp_finish(RpCounters *cnt, const uint8_t *flag, uint32_t *result) {
+    const uint32_t m = cnt->m;
+    result[0] = cnt->nvis;
+    result[1] = flag[m + 1] ? 1u : 0u;  // the path ends in an error (unexpected EOF)
+    result[2] = cnt->ncand;
+    result[3] = m;
+}
+
+// ---- Getvhash (store/item.go:89-100) with the sign-extending Fnv1a (utils/hash.go:8-16) ----
+__device__ __forceinline__ uint32_t fnv1a_bytes(const uint8_t *p, uint32_t n, uint32_t h) {
+    for (uint32_t i = 0; i < n; i++) {
+        h ^= (uint32_t)(int32_t)(int8_t)p[i];
+        h *= 0x01000193u;
+    }
+    return h;
+}
+
+__global__ void __launch_bounds__(64) k_vhash(const uint8_t *src, const uint64_t *off, const uint32_t *len,
+                                              uint32_t n, uint16_t *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *v = src + off[i];
+    const uint32_t l = len[i];
+    uint32_t h = l * 97u;
+    if (l <= 1024) {
+        h += fnv1a_bytes(v, l, 0x811c9dc5u);
+    } else {
+        h += fnv1a_bytes(v, 512, 0x811c9dc5u);
+        h *= 97u;
+        h += fnv1a_bytes(v + l - 512, 512, 0x811c9dc5u);
+    }
+    out[i] = (uint16_t)h;
+}
+
+// ---- workspace layout ----
+struct RpWs {
+    RpCounters *cnt;
+    uint8_t *kind, *flag;
+    uint32_t *rsz, *cand, *vidx, *A, *J, *J2, *vis, *tiles;
+};
+
+inline size_t rp_align(size_t x) { return (x + 255) & ~(size_t)255; }
+
+inline size_t replay_ws_layout(uint64_t size, uint8_t *base, RpWs *w) {
+    const uint64_t ns = (size + kRpSlot - 1) / kRpSlot;
+    const size_t n = (size_t)ns + 2;
+    const size_t ntiles = (n + kScanTile - 1) / kScanTile;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        uint8_t *p = base ? base + o : nullptr;
+        o += rp_align(bytes);
+        return p;
+    };
+    RpWs t;
+    t.cnt = (RpCounters *)take(sizeof(RpCounters));
+    t.kind = take(n);
+    t.flag = take(n);
+    t.rsz = (uint32_t *)take(4 * n);
+    t.cand = (uint32_t *)take(4 * n);
+    t.vidx = (uint32_t *)take(4 * n);
+    t.A = (uint32_t *)take(4 * n);
+    t.J = (uint32_t *)take(4 * n);
+    t.J2 = (uint32_t *)take(4 * n);
+    t.vis = (uint32_t *)take(4 * n);
+    t.tiles = (uint32_t *)take(4 * (ntiles + 1));
+    if (w) *w = t;
+    return o;
+}
+
+inline int launch_replay_index(const uint8_t *data, uint64_t size, uint64_t start, uint32_t max_key,
+                               uint64_t body_max, uint64_t *rec_off, uint32_t *rec_broken, uint32_t *result,
+                               void *ws, hipStream_t s) {
+    RpWs w;
+    replay_ws_layout(size, (uint8_t *)ws, &w);
+    const uint32_t nslots = (uint32_t)((size + kRpSlot - 1) / kRpSlot);
+    const uint32_t n2 = nslots + 2;
+    const uint32_t ntiles = (n2 + kScanTile - 1) / kScanTile;
+    const uint32_t g256 = (n2 + 255) / 256;
+    hipError_t e = hipMemsetAsync(w.cnt, 0, sizeof(RpCounters), s);
+    if (e != hipSuccess) return (int)e;
+    if (nslots)
+        hipLaunchKernelGGL(k_rp_slots, dim3((nslots + 255) / 256), dim3(256), 0, s, data, size, nslots, max_key,
+                           body_max, w.kind, w.rsz, w.cand, w.cnt);
+    const uint32_t crc_grid = nslots / 4 + 1 < 65536 ? nslots / 4 + 1 : 65536;
+    hipLaunchKernelGGL(k_rp_crc, dim3(crc_grid), dim3(256), 0, s, data, w.cand, w.cnt, w.rsz);
+    // valid slots in order: vidx (exclusive count) and A
+    ValidFlag vf{w.rsz};
+    hipLaunchKernelGGL(k_scan_tiles<ValidFlag>, dim3(ntiles), dim3(256), 0, s, vf, nslots, w.tiles);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, w.tiles, ntiles, &w.cnt->m);
+    hipLaunchKernelGGL((k_scan_apply<ValidFlag, ScatterValid>), dim3(ntiles), dim3(256), 0, s, vf,
+                       ScatterValid{w.vidx, w.A}, nslots, w.tiles);
+    // successors, start, and the path by pointer doubling
+    hipLaunchKernelGGL(k_rp_next, dim3(g256), dim3(256), 0, s, size, nslots, start, w.kind, w.rsz, w.vidx, w.A,
+                       w.cnt, w.J, w.flag);
+    hipLaunchKernelGGL(k_rp_seed, dim3(1), dim3(1), 0, s, w.cnt, w.flag);
+    uint32_t *J = w.J, *J2 = w.J2;
+    for (uint64_t reach = 1; reach < (uint64_t)n2 + 1; reach <<= 1) {
+        hipLaunchKernelGGL(k_rp_double, dim3(g256), dim3(256), 0, s, w.cnt, J, J2, w.flag);
+        uint32_t *t = J; J = J2; J2 = t;
+    }
+    // visited records in order
+    VisitFlag ff{w.flag, w.cnt};
+    hipLaunchKernelGGL(k_scan_tiles<VisitFlag>, dim3(ntiles), dim3(256), 0, s, ff, nslots, w.tiles);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, w.tiles, ntiles, &w.cnt->nvis);
+    hipLaunchKernelGGL((k_scan_apply<VisitFlag, ScatterVisit>), dim3(ntiles), dim3(256), 0, s, ff,
+                       ScatterVisit{w.A, w.vis}, nslots, w.tiles);
+    hipLaunchKernelGGL(k_rp_emit, dim3((nslots + 255) / 256 + 1), dim3(256), 0, s, w.vis, w.cnt, w.rsz, start,
+                       rec_off, rec_broken);
+    hipLaunchKernelGGL(k_rp_finish, dim3(1), dim3(1), 0, s, w.cnt, w.flag, result);
+    e = hipGetLastError();
+    return (int)e;
+}
+
+}  // namespace qlzx

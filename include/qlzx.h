@@ -135,6 +135,27 @@ int qlzx_synth_batch(int kind, uint64_t seed, uint64_t first_id, uint8_t *dst,
                      const uint8_t *vocab, const uint32_t *vocab_off, const uint32_t *zipf_cdf,
                      uint32_t nwords, void *stream);
 
+/* ---- .data chunk replay ----
+ * Replaces the DataStreamReader.Next loop of buildHintFromData
+ * (store/datafile.go:202-277, store/bucket.go:89-117) over one chunk file that
+ * is resident in device memory: the records the sequential reader would
+ * return from `start` (a multiple of 256), in order, each with its offset and
+ * sizeBroken (bytes skipped by the nextValid resync).  CRCs are verified
+ * (store/datafile.go:161-168) as part of record discovery.
+ *   max_key  MaxKeyLen (config/mc_config.go:6, 250); body_max BodyMax (50 MiB)
+ *   rec_off / rec_broken: capacity size/256 + 1 entries
+ *   result[0] = records found; result[1] = 1 if the reader stops on an error
+ *   (unexpected EOF: partial header or truncated record) after them;
+ *   result[2] = header-plausible slots, result[3] = CRC-valid slots. */
+size_t qlzx_replay_workspace_size(uint64_t size);
+int qlzx_replay_index(const uint8_t *data, uint64_t size, uint64_t start, uint32_t max_key, uint64_t body_max,
+                      uint64_t *rec_off, uint32_t *rec_broken, uint32_t *result, void *workspace,
+                      size_t workspace_bytes, void *stream);
+
+/* Getvhash (store/item.go:89-100, Fnv1a of utils/hash.go:8-16) of n values. */
+int qlzx_vhash_batch(const uint8_t *src, const uint64_t *off, const uint32_t *len, uint32_t n, uint16_t *out,
+                     void *stream);
+
 /* Last error message of the calling thread (empty if none). */
 const char *qlzx_last_error(void);
 

@@ -1,0 +1,111 @@
+"""GPU .data replay (record discovery + nextValid resync + CRC + decompress + Getvhash)
+against the sequential restatement in oracle/replay.py."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from oracle import replay as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu(data: bytes, start=0, **kw):
+    from gobeansdb_amd import replay
+    t = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda() if data else \
+        torch.zeros(0, dtype=torch.uint8, device="cuda")
+    res = replay.replay(t, start=start, **kw)
+    torch.cuda.synchronize()
+    vals = res.values
+    host = vals.data.cpu().numpy()
+    voff = vals.off.cpu().numpy().view(np.uint64)
+    rows = []
+    offs = res.offset.cpu().numpy()
+    brk = res.size_broken.cpu().numpy()
+    hdr = res.header.cpu().numpy()
+    flag = res.flag.cpu().numpy().view(np.uint32)
+    vlen = res.value_len.cpu().numpy()
+    vh = res.vhash.cpu().numpy()
+    comp = (hdr[:, 2].view(np.uint32) & R.FLAG_COMPRESS) != 0 if len(hdr) else np.zeros(0, bool)
+    ci = 0
+    for k in range(res.n):
+        off = int(offs[k])
+        ksz = int(hdr[k, 4])
+        key = data[off + 24: off + 24 + ksz]
+        if comp[k] and (flag[k] & R.FLAG_COMPRESS) == 0:
+            o = int(voff[ci])
+            body = host[o: o + int(vlen[k])].tobytes()
+        else:
+            body = data[off + 24 + ksz: off + 24 + ksz + int(vlen[k])]
+        if comp[k]:
+            ci += 1
+        rows.append((off, int(brk[k]), key, int(hdr[k, 3]), int(flag[k]), body, int(vh[k])))
+    return rows, res.end_error
+
+
+def _check(data, start=0):
+    exp_rows, exp_err = R.replay(data, start)
+    got_rows, got_err = _gpu(data, start)
+    assert len(got_rows) == len(exp_rows)
+    for g, e in zip(got_rows, exp_rows):
+        assert g == e
+    assert got_err == (exp_err is not None)
+
+
+def test_data_broken(cuda):
+    from tests.test_replay_oracle import _data_broken_file
+    data = _data_broken_file()
+    rows, err = _gpu(data)
+    assert [(r[0], r[1], r[5]) for r in rows[:2]] == [(8 * 256, 8 * 256, b"value_5"), (9 * 256, 0, b"value_6")]
+    _check(data)
+
+
+def test_golden_records(cuda, golden):
+    _check(golden.records_data)
+
+
+def _random_file(rng: random.Random, nrec: int):
+    out = b""
+    for i in range(nrec):
+        n = int(np.exp(rng.uniform(np.log(5), np.log(40000))))
+        val = O.gen_text(rng.getrandbits(32), i, n) if rng.random() < 0.7 else O.gen_image(rng.getrandbits(32), i, n)
+        key = b"key_%016x" % rng.getrandbits(64)
+        flag = 0
+        if n > 256 and rng.random() < 0.6:
+            c = O.compress(val)
+            if len(c) < 0.9 * n:
+                val, flag = c, R.FLAG_COMPRESS
+        out += R.make_record(key, val, flag=flag, ver=rng.randrange(-3, 100), ts=rng.getrandbits(32))
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_random_files_with_corruption(cuda, seed):
+    rng = random.Random(seed)
+    data = bytearray(_random_file(rng, 60))
+    _check(bytes(data))
+    for _ in range(12):  # header fields, key and value bytes, padding
+        p = rng.randrange(len(data))
+        data[p] = rng.getrandbits(8)
+    _check(bytes(data))
+    # a record with a broken compressed body (CRC recomputed so it is found): decompress fails,
+    # the body stays compressed (store/item.go:167-170)
+    bad = R.make_record(b"kbad", b"\x4f" + bytes(40), flag=R.FLAG_COMPRESS)
+    _check(bytes(data) + bad)
+    # truncations: inside a header, inside a body
+    cut = rng.randrange(len(data))
+    _check(bytes(data[:cut]))
+    _check(bytes(data[: (cut // 256) * 256 + 10]))
+
+
+def test_start_offset_and_edges(cuda):
+    rng = random.Random(9)
+    data = _random_file(rng, 20)
+    rows, _ = R.replay(data)
+    _check(data, start=rows[5][0])
+    _check(data, start=rows[5][0] + 256)   # lands inside a record: resync
+    _check(b"")
+    _check(bytes(4096))                     # all zero: no record, clean end
+    _check(bytes(100))                      # partial header
