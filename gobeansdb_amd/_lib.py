@@ -80,6 +80,10 @@ def lib() -> ctypes.CDLL:
     L.qlzx_crc32_batch.restype = ctypes.c_int
     L.qlzx_synth_batch.argtypes = [ctypes.c_int, u64, u64, vp, vp, vp, u32, vp, vp, vp, u32, vp]
     L.qlzx_synth_batch.restype = ctypes.c_int
+    L.qlzx_crc32_combine.argtypes = [vp, vp, vp, u32, u32, vp, vp]
+    L.qlzx_crc32_combine.restype = ctypes.c_int
+    L.qlzx_copy_batch.argtypes = [vp, vp, vp, vp, vp, u32, vp]
+    L.qlzx_copy_batch.restype = ctypes.c_int
     L.qlzx_replay_workspace_size.argtypes = [u64]
     L.qlzx_replay_workspace_size.restype = sz
     L.qlzx_replay_index.argtypes = [vp, u64, u64, u32, u64, vp, vp, vp, vp, sz, vp]

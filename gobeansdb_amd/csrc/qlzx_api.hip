@@ -17,6 +17,7 @@
 #include "qlzx_encode_wg.hip"
 #include "qlzx_crc.hip"
 #include "qlzx_replay.hip"
+#include "qlzx_record.hip"
 
 namespace {
 
@@ -177,6 +178,26 @@ int qlzx_synth_batch(int kind, uint64_t seed, uint64_t first_id, uint8_t *dst, c
         return fail(QLZX_R_BAD_ARG, "qlzx_synth_batch: null arg");
     hipLaunchKernelGGL(qlzx::k_synth, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, kind, seed,
                        first_id, dst, dst_off, len, n, vocab, vocab_off, zipf_cdf, nwords);
+    HIP_OK(hipGetLastError());
+    return QLZX_R_OK;
+}
+
+int qlzx_crc32_combine(const uint32_t *raw_a, const uint32_t *raw_b, const uint32_t *len_b, uint32_t n,
+                       uint32_t final_xor, uint32_t *out, void *stream) {
+    if (n == 0) return QLZX_R_OK;
+    if (!raw_a || !raw_b || !len_b || !out) return fail(QLZX_R_BAD_ARG, "qlzx_crc32_combine: null arg");
+    hipLaunchKernelGGL(qlzx::k_crc_combine, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, raw_a, raw_b,
+                       len_b, n, final_xor, out);
+    HIP_OK(hipGetLastError());
+    return QLZX_R_OK;
+}
+
+int qlzx_copy_batch(const uint8_t *src, const uint64_t *src_off, const uint32_t *len, uint8_t *dst,
+                    const uint64_t *dst_off, uint32_t n, void *stream) {
+    if (n == 0) return QLZX_R_OK;
+    if (!src || !src_off || !len || !dst || !dst_off) return fail(QLZX_R_BAD_ARG, "qlzx_copy_batch: null arg");
+    hipLaunchKernelGGL(qlzx::k_copy_blocks, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, src, src_off, len,
+                       dst, dst_off, n);
     HIP_OK(hipGetLastError());
     return QLZX_R_OK;
 }

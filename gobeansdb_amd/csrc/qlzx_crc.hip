@@ -14,19 +14,41 @@ namespace qlzx {
 constexpr uint32_t kStripe = 4096;
 constexpr uint32_t kPiece = 64;
 
-// Raw CRC from state 0 of `len` bytes at p, wave-cooperative; all lanes return the result.
-__device__ uint32_t wave_crc_raw(const uint32_t *tab, const uint8_t *p, uint64_t len, uint32_t lane) {
+// Raw CRC from state 0 of `len` bytes at p, wave-cooperative; all lanes return
+// the result.  t8 = slicing-by-8 tables in LDS.  Full 4-KiB stripes: lane l
+// runs slicing-by-8 over its 64-B piece (16-B loads when p is 4-aligned), then
+// crc(stripe) = XOR_l piece_crc_l * x^(8*64*(63-l)) (one GF(2) product per
+// lane, g_crc_piece) and run = run * x^(8*4096) ^ crc(stripe).  The last,
+// partial stripe takes the byte path with a general shift.
+__device__ uint32_t wave_crc_raw(const uint32_t *t8, const uint8_t *p, uint64_t len, uint32_t lane) {
     uint32_t run = 0;
-    for (uint64_t base = 0; base < len; base += kStripe) {
-        const uint32_t slen = (uint32_t)((len - base) < kStripe ? (len - base) : kStripe);
+    const bool al4 = (((uintptr_t)p) & 3u) == 0;
+    const uint32_t kshift = g_crc_piece[63 - lane];
+    const uint32_t kstripe = g_crc_pow[12];  // x^(8 * 4096)
+    uint64_t base = 0;
+    for (; base + kStripe <= len; base += kStripe) {
+        const uint8_t *q = p + base + lane * kPiece;
+        uint32_t c = 0;
+        if (al4) {
+            const uint32_t *w = (const uint32_t *)q;
+#pragma unroll
+            for (int k = 0; k < 16; k += 2) c = crc_slice8(t8, c, w[k], w[k + 1]);
+        } else {
+            for (uint32_t k = 0; k < kPiece; k++) c = crc_byte(t8, c, q[k]);
+        }
+        c = gf2_mulmod(kshift, c);
+        for (int m = 32; m >= 1; m >>= 1) c ^= __shfl_xor(c, m, 64);
+        run = gf2_mulmod(kstripe, run) ^ c;
+    }
+    if (base < len) {  // partial stripe
+        const uint32_t slen = (uint32_t)(len - base);
         const uint32_t lo = lane * kPiece;
-        uint32_t c = 0, mine = 0;
+        uint32_t c = 0;
         if (lo < slen) {
-            mine = (slen - lo) < kPiece ? (slen - lo) : kPiece;
+            const uint32_t mine = (slen - lo) < kPiece ? (slen - lo) : kPiece;
             const uint8_t *q = p + base + lo;
-            for (uint32_t k = 0; k < mine; k++) c = crc_byte(tab, c, q[k]);
-            const uint32_t after = slen - lo - mine;
-            c = crc_shift(c, after);
+            for (uint32_t k = 0; k < mine; k++) c = crc_byte(t8, c, q[k]);
+            c = crc_shift(c, slen - lo - mine);
         }
         for (int m = 32; m >= 1; m >>= 1) c ^= __shfl_xor(c, m, 64);
         run = crc_shift(run, slen) ^ c;
@@ -38,8 +60,8 @@ __global__ void __launch_bounds__(256) k_crc32(const uint8_t *src, const uint64_
                                                const uint32_t *len, uint32_t n,
                                                const uint32_t *init, uint32_t final_xor,
                                                uint32_t *out) {
-    __shared__ uint32_t tab[256];
-    load_crc_table(tab);
+    __shared__ uint32_t tab[8 * 256];
+    load_crc_slice8(tab);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t i = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;

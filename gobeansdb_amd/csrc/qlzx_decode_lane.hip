@@ -88,8 +88,8 @@ __global__ void __launch_bounds__(256) k_decode_lane(qlzx_blocks b, const uint32
         if (len >= hb && parse_header(src).dsize < min_dsize) return;  // owned by the fast path
     }
     int st = QLZX_OK;
-    if (crc_state) {  // record CRC over the stored (compressed) value bytes
-        uint32_t c = crc_state[i];
+    if (crc_state || crc_expect || crc_out) {  // record CRC over the stored (compressed) value bytes
+        uint32_t c = crc_state ? crc_state[i] : 0xffffffffu;
         for (uint32_t k = 0; k < len; k++) c = crc_byte(tab, c, src[k]);
         c = ~c;
         if (crc_out) crc_out[i] = c;

@@ -68,8 +68,9 @@ inline bool decode_wave_enabled() { return true; }
 inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
     const uint32_t md = max_dsize > QLZX_FAST_MAX_DSIZE ? QLZX_FAST_MAX_DSIZE : max_dsize;
     const uint32_t c = n < kChunkBlocks ? (n ? n : 1) : kChunkBlocks;
-    return (((size_t)c * sizeof(BlkInfo) + 255) & ~(size_t)255) + (size_t)c * groups_max(md) * sizeof(GroupRec) +
-           256;
+    return (((size_t)c * sizeof(BlkInfo) + 255) & ~(size_t)255) +
+           ((((size_t)c * groups_max(md) * sizeof(GroupRec)) + 255) & ~(size_t)255) +
+           (((size_t)3 * c * sizeof(uint32_t) + 255) & ~(size_t)255) + 256;
 }
 
 // ------------------------------------------------------------------ K1 ----
@@ -375,11 +376,11 @@ __device__ __forceinline__ uint32_t ff1_or(uint64_t m, uint32_t dflt) {
 template <uint32_t MAXD>
 __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                                                    uint32_t first, uint32_t count, const BlkInfo *info,
-                                                   const GroupRec *recs, uint32_t gmax) {
+                                                   const GroupRec *recs, uint32_t gmax, const uint32_t *list) {
     __shared__ __attribute__((aligned(16))) K2Lds<MAXD> L;
     const uint32_t lane = threadIdx.x;
-    const uint32_t li = blockIdx.x;
-    if (li >= count) return;
+    if (blockIdx.x >= count) return;
+    const uint32_t li = list ? list[blockIdx.x] : blockIdx.x;  // block of the chunk (size-class list)
     const uint32_t i = first + li;
     const BlkInfo bi = info[li];
     if (bi.kind == kBlkSkip) return;
@@ -566,6 +567,18 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
     }
 }
 
+// Size classes for mixed batches: K2<16384> (9 WGs/CU), K2<32768>, K2<65536>.
+constexpr uint32_t kClasses = 3;
+__global__ void __launch_bounds__(256) k_dec_classify(const BlkInfo *info, uint32_t count, uint32_t *lists,
+                                                      uint32_t *counts) {
+    const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= count) return;
+    const BlkInfo bi = info[li];
+    if (bi.kind == kBlkSkip) return;
+    const uint32_t c = bi.dsize <= 16384 ? 0u : (bi.dsize <= 32768 ? 1u : 2u);
+    lists[(size_t)c * count + atomicAdd(&counts[c], 1u)] = li;
+}
+
 inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uint32_t *dsize,
                               int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
                               uint32_t *crc_out, uint32_t max_dsize, void *ws, size_t ws_bytes,
@@ -575,7 +588,16 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     const uint32_t gmax = groups_max(md);
     const uint32_t chunk = b.n < kChunkBlocks ? b.n : kChunkBlocks;
     BlkInfo *info = (BlkInfo *)ws;
-    GroupRec *recs = (GroupRec *)((uint8_t *)ws + (((size_t)chunk * sizeof(BlkInfo) + 255) & ~(size_t)255));
+    const size_t o_rec = ((size_t)chunk * sizeof(BlkInfo) + 255) & ~(size_t)255;
+    GroupRec *recs = (GroupRec *)((uint8_t *)ws + o_rec);
+    const size_t o_lists = o_rec + ((((size_t)chunk * gmax * sizeof(GroupRec)) + 255) & ~(size_t)255);
+    uint32_t *cls_lists = (uint32_t *)((uint8_t *)ws + o_lists);
+    uint32_t *cls_counts = (uint32_t *)((uint8_t *)ws + o_lists + ((((size_t)3 * chunk * 4) + 255) & ~(size_t)255));
+    static thread_local uint32_t *h_counts = nullptr;  // pinned, for the class counts
+    if (md > 16384 && !h_counts) {
+        hipError_t e = hipHostMalloc((void **)&h_counts, 64, hipHostMallocDefault);
+        if (e != hipSuccess) return (int)e;
+    }
     const bool crc = crc_state || crc_expect || crc_out;
     for (uint32_t first = 0; first < b.n; first += chunk) {
         const uint32_t cnt = b.n - first < chunk ? b.n - first : chunk;
@@ -585,12 +607,29 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         else
             hipLaunchKernelGGL(k_dec_parse<false>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s, b,
                                dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax);
-        if (md <= 16384)
+        if (md <= 16384) {
             hipLaunchKernelGGL(k_dec_blocks<16384>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
-                               recs, gmax);
-        else
-            hipLaunchKernelGGL(k_dec_blocks<QLZX_FAST_MAX_DSIZE>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first,
-                               cnt, info, recs, gmax);
+                               recs, gmax, (const uint32_t *)nullptr);
+        } else {
+            // mixed sizes: route every block to the smallest K2 whose LDS history holds it
+            hipError_t e = hipMemsetAsync(cls_counts, 0, kClasses * sizeof(uint32_t), s);
+            if (e != hipSuccess) return (int)e;
+            hipLaunchKernelGGL(k_dec_classify, dim3((cnt + 255) / 256), dim3(256), 0, s, info, cnt, cls_lists,
+                               cls_counts);
+            e = hipMemcpyAsync(h_counts, cls_counts, kClasses * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return (int)e;
+            if (h_counts[0])
+                hipLaunchKernelGGL(k_dec_blocks<16384>, dim3(h_counts[0]), dim3(64), 0, s, b, dsize, status, first,
+                                   h_counts[0], info, recs, gmax, (const uint32_t *)cls_lists);
+            if (h_counts[1])
+                hipLaunchKernelGGL(k_dec_blocks<32768>, dim3(h_counts[1]), dim3(64), 0, s, b, dsize, status, first,
+                                   h_counts[1], info, recs, gmax, (const uint32_t *)(cls_lists + cnt));
+            if (h_counts[2])
+                hipLaunchKernelGGL(k_dec_blocks<QLZX_FAST_MAX_DSIZE>, dim3(h_counts[2]), dim3(64), 0, s, b, dsize,
+                                   status, first, h_counts[2], info, recs, gmax,
+                                   (const uint32_t *)(cls_lists + 2 * (size_t)cnt));
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }

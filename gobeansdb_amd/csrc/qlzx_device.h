@@ -26,6 +26,8 @@ extern __device__ uint32_t g_crc_table[256];
 extern __device__ uint32_t g_crc_pow[64];
 // g_crc_slice8[k * 256 + b]: CRC of byte b followed by k zero bytes (slicing-by-8).
 extern __device__ uint32_t g_crc_slice8[8 * 256];
+// g_crc_piece[k] = x^(8 * 64 * k) mod P: shift of a 64-B piece's CRC over k later 64-B pieces.
+extern __device__ uint32_t g_crc_piece[64];
 
 constexpr uint32_t CRC_POLY = 0xEDB88320u;
 
@@ -61,6 +63,11 @@ __device__ __forceinline__ uint32_t crc_word(const uint32_t *tab, uint32_t c, ui
     c = crc_byte(tab, c, (w >> 8) & 0xff);
     c = crc_byte(tab, c, (w >> 16) & 0xff);
     return crc_byte(tab, c, w >> 24);
+}
+
+// Load the slicing-by-8 tables into LDS (call by the whole block, then __syncthreads()).
+__device__ __forceinline__ void load_crc_slice8(uint32_t *lds_tab8) {
+    for (uint32_t i = threadIdx.x; i < 8 * 256; i += blockDim.x) lds_tab8[i] = g_crc_slice8[i];
 }
 
 // Load the CRC table into LDS (call by the whole block, then __syncthreads()).

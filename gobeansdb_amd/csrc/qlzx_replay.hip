@@ -63,8 +63,8 @@ __device__ uint32_t wave_crc_raw(const uint32_t *tab, const uint8_t *p, uint64_t
 
 __global__ void __launch_bounds__(256) k_rp_crc(const uint8_t *data, const uint32_t *cand,
                                                 const RpCounters *cnt, uint32_t *rsz) {
-    __shared__ uint32_t tab[256];
-    load_crc_table(tab);
+    __shared__ uint32_t tab[8 * 256];
+    load_crc_slice8(tab);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nc = cnt->ncand;

@@ -6,6 +6,7 @@ namespace qlzx {
 struct CrcTables {
     uint32_t table[256];
     uint32_t pow8[64];
+    uint32_t piece[64];  // piece[k] = x^(8 * 64 * k): shifts a 64-B piece's CRC over k later pieces
     uint32_t slice[8][256];  // slice[k][b]: CRC of byte b followed by k zero bytes (slicing-by-8)
 };
 
@@ -39,6 +40,8 @@ __host__ __device__ constexpr CrcTables make_tables() {
         t.pow8[k] = x;  // x^(8 * 2^k)
         x = mulmod_c(x, x);
     }
+    t.piece[0] = 0x80000000u;  // x^0
+    for (int k = 1; k < 64; k++) t.piece[k] = mulmod_c(t.piece[k - 1], t.pow8[6]);  // * x^(8*64)
     return t;
 }
 
@@ -74,6 +77,14 @@ __device__ uint32_t g_crc_pow[64] = {
     P8(0), P8(8), P8(16), P8(24), P8(32), P8(40), P8(48), P8(56)
 #undef P8
 #undef P
+};
+
+__device__ uint32_t g_crc_piece[64] = {
+#define Q(i) kTables.piece[i]
+#define Q8(i) Q(i), Q(i + 1), Q(i + 2), Q(i + 3), Q(i + 4), Q(i + 5), Q(i + 6), Q(i + 7)
+    Q8(0), Q8(8), Q8(16), Q8(24), Q8(32), Q8(40), Q8(48), Q8(56)
+#undef Q8
+#undef Q
 };
 
 }  // namespace qlzx

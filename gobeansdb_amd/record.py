@@ -1,0 +1,201 @@
+"""Write-side record encode on the GPU.
+
+Host mirror of the set path between a value arriving and its bytes reaching a
+.data chunk:
+
+  Record.TryCompress     store/item.go:120-161  (policy: ver >= 0, no client /
+                         compress flag, padded record > 256 B, MIME sniff, a
+                         10 KiB trial compress kept when float32(c)/float32(t) <= 0.7,
+                         then the whole body)
+  NeedCompress           store/item.go:114-118 + NotCompress defaults
+                         (store/config_default.go:46-49: audio/wave, audio/mpeg)
+  WriteRecord.encodeHeader / getCRC / append   store/datafile.go:66-88, 307-330
+
+The compress runs in qlzx_compress_batch with the value CRC fused (raw state 0),
+and the header+key prefix is folded in with qlzx_crc32_combine, because the
+header carries the compressed size.  Records come out 256-B padded and laid
+out back to back, ready to append.
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib, batch
+
+FLAG_COMPRESS = 0x00010000
+FLAG_CLIENT_COMPRESS = 0x00000010
+TRY_COMPRESS_SIZE = 10 * 1024
+COMPRESS_RATIO_LIMIT = np.float32(0.7)
+PADDING = 256
+HDR = 24
+NOT_COMPRESS = frozenset({"audio/wave", "audio/mpeg"})
+
+
+def sniff(prefix: bytes) -> str | None:
+    """The two http.DetectContentType answers NeedCompress can act on.  Their
+    signatures ("ID3"; "RIFF" ???? "WAVE") cannot be shadowed by an earlier rule
+    of the sniff table (HTML/XML need '<' after whitespace, the other binary
+    signatures differ in their first bytes; RIFF/WEBP differs at offset 8)."""
+    p = prefix[:512]
+    if p[:3] == b"ID3":
+        return "audio/mpeg"
+    if p[:4] == b"RIFF" and p[8:12] == b"WAVE":
+        return "audio/wave"
+    return None
+
+
+def need_compress(prefix: bytes, not_compress=NOT_COMPRESS) -> bool:
+    """store/item.go:114-118."""
+    return sniff(prefix) not in not_compress
+
+
+@dataclass
+class Encoded:
+    data: torch.Tensor        # uint8 device buffer: the records, back to back
+    offset: np.ndarray        # uint64 record offsets
+    flag: np.ndarray          # uint32 flags as written (FLAG_COMPRESS added where kept)
+    vsz: np.ndarray           # uint32 stored value sizes
+    crc: np.ndarray           # uint32 record CRCs
+
+
+def _dev_u64(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).to(dev)
+
+
+def _dev_u32(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(dev)
+
+
+def encode(keys: list[bytes], values: batch.BlockBatch, flags=None, vers=None, ts=None,
+           not_compress=NOT_COMPRESS, workspace: batch.Workspace | None = None, stream=None) -> Encoded:
+    """TryCompress + encodeHeader + padding for n records whose values live on the device."""
+    L = _lib.lib()
+    dev = values.data.device
+    n = values.n
+    ws = workspace or batch.Workspace(dev)
+    flags = np.zeros(n, np.uint32) if flags is None else np.asarray(flags, np.uint32).copy()
+    vers = np.zeros(n, np.int32) if vers is None else np.asarray(vers, np.int32)
+    ts = np.zeros(n, np.uint32) if ts is None else np.asarray(ts, np.uint32)
+    vlen = values.length.cpu().numpy().view(np.uint32).astype(np.int64)
+    voff = values.off.cpu().numpy().view(np.uint64)
+    klen = np.asarray([len(k) for k in keys], np.int64)
+
+    # ---- TryCompress candidates (store/item.go:121-137) ----
+    padded = (HDR + klen + vlen + 255) // 256 * 256
+    cand = (vers >= 0) & ((flags & (FLAG_CLIENT_COMPRESS | FLAG_COMPRESS)) == 0) & (padded > PADDING)
+    ci = np.nonzero(cand)[0]
+    if len(ci):
+        # sniff the first 512 bytes of each candidate (gathered from the device)
+        heads = _gather_prefix(values, ci, 512)
+        ok = np.asarray([need_compress(h, not_compress) for h in heads], bool)
+        ci = ci[ok]
+    comp_body = {}   # record -> (device buffer, offset, length, raw value crc)
+    if len(ci):
+        tlen = np.minimum(vlen[ci], TRY_COMPRESS_SIZE)
+        trial = batch.BlockBatch(values.data, _dev_u64(voff[ci], dev), _dev_u32(tlen, dev))
+        crc0 = torch.zeros(len(ci), dtype=torch.int32, device=dev)
+        tdst, tcs, tst, tcrc = batch.compress(trial, crc_state=crc0, max_len=int(tlen.max()), workspace=ws,
+                                             stream=stream)
+        tcs_h = tcs.cpu().numpy().view(np.uint32).astype(np.int64)
+        if int((tst != 0).sum()):
+            raise _lib.QlzxError("trial compress failed on the device")
+        keep = (tcs_h.astype(np.float32) / tlen.astype(np.float32)) <= COMPRESS_RATIO_LIMIT   # :145
+        tcrc_h = tcrc.cpu().numpy().view(np.uint32)
+        toff_h = tdst.off.cpu().numpy().view(np.uint64)
+        full = keep & (vlen[ci] > tlen)      # :149-156: recompress the whole body
+        for j in np.nonzero(keep & ~full)[0]:
+            comp_body[int(ci[j])] = (tdst.data, int(toff_h[j]), int(tcs_h[j]), int(tcrc_h[j]) ^ 0xFFFFFFFF)
+        fi = ci[full]
+        if len(fi):
+            fsrc = batch.BlockBatch(values.data, _dev_u64(voff[fi], dev), _dev_u32(vlen[fi], dev))
+            fcrc0 = torch.zeros(len(fi), dtype=torch.int32, device=dev)
+            fdst, fcs, fst, fcrc = batch.compress(fsrc, crc_state=fcrc0, max_len=int(vlen[fi].max()),
+                                                 workspace=ws, stream=stream)
+            if int((fst != 0).sum()):
+                raise _lib.QlzxError("compress failed on the device")
+            fcs_h = fcs.cpu().numpy().view(np.uint32).astype(np.int64)
+            fcrc_h = fcrc.cpu().numpy().view(np.uint32)
+            foff_h = fdst.off.cpu().numpy().view(np.uint64)
+            for j, r in enumerate(fi):
+                comp_body[int(r)] = (fdst.data, int(foff_h[j]), int(fcs_h[j]), int(fcrc_h[j]) ^ 0xFFFFFFFF)
+    # ---- stored value sizes / flags ----
+    vsz = vlen.copy()
+    for r, (_, _, cl, _) in comp_body.items():
+        vsz[r] = cl
+        flags[r] += FLAG_COMPRESS                                   # :159
+    # ---- raw CRC (from state 0) of every stored value ----
+    raw_v = np.zeros(n, np.uint32)
+    plain = np.asarray([r for r in range(n) if r not in comp_body], np.int64)
+    if len(plain):
+        c = batch.crc32(batch.BlockBatch(values.data, _dev_u64(voff[plain], dev), _dev_u32(vlen[plain], dev)),
+                        init=torch.zeros(len(plain), dtype=torch.int32, device=dev), final_xor=0, stream=stream)
+        raw_v[plain] = c.cpu().numpy().view(np.uint32)
+    for r, (_, _, _, rc) in comp_body.items():
+        raw_v[r] = rc
+    # ---- header[4:24] ‖ key prefixes, their raw CRC state from ~0, and the combine ----
+    pre = bytearray()
+    pre_off = np.zeros(n, np.uint64)
+    for r in range(n):
+        pre_off[r] = len(pre)
+        pre += struct.pack("<IIiII", int(ts[r]), int(flags[r]), int(vers[r]), int(klen[r]), int(vsz[r])) + keys[r]
+        pre += bytes((-len(pre)) % 16)
+    pre_d = torch.from_numpy(np.frombuffer(bytes(pre), np.uint8).copy()).to(dev)
+    pre_len = (20 + klen).astype(np.uint32)
+    s_hk = batch.crc32(batch.BlockBatch(pre_d, _dev_u64(pre_off, dev), _dev_u32(pre_len, dev)), final_xor=0,
+                       stream=stream)
+    crc_d = torch.zeros(n, dtype=torch.int32, device=dev)
+    rv = _dev_u32(raw_v, dev)
+    lv = _dev_u32(vsz, dev)
+    _lib.check(L.qlzx_crc32_combine(s_hk.data_ptr(), rv.data_ptr(), lv.data_ptr(), n, 0xFFFFFFFF,
+                                    crc_d.data_ptr(), batch._stream(stream)), "qlzx_crc32_combine")
+    crc = crc_d.cpu().numpy().view(np.uint32).copy()
+    # ---- assemble: crc ‖ header tail ‖ key ‖ value, zero padding to 256 (datafile.go:307-330) ----
+    rsize = (HDR + klen + vsz + 255) // 256 * 256
+    roff = np.zeros(n, np.uint64)
+    if n:
+        roff[1:] = np.cumsum(rsize)[:-1]
+    total = int(rsize.sum())
+    out = torch.zeros(max(total, 1), dtype=torch.uint8, device=dev)
+    # header tail + key (from the prefix staging) at off + 4
+    _copy(pre_d, pre_off, pre_len, out, roff + 4, stream)
+    # values: raw ones from the value buffer, compressed ones from their compress buffers
+    if len(plain):
+        _copy(values.data, voff[plain], vlen[plain].astype(np.uint32), out,
+              roff[plain] + HDR + klen[plain].astype(np.uint64), stream)
+    by_buf = {}
+    for r, (buf, o, cl, _) in comp_body.items():
+        by_buf.setdefault(id(buf), (buf, []))[1].append((r, o, cl))
+    for buf, lst in by_buf.values():
+        rs = np.asarray([t[0] for t in lst], np.int64)
+        _copy(buf, np.asarray([t[1] for t in lst], np.uint64), np.asarray([t[2] for t in lst], np.uint32), out,
+              roff[rs] + HDR + klen[rs].astype(np.uint64), stream)
+    # crc field (records are 256-B aligned, so int32 words)
+    out.view(torch.int32)[torch.from_numpy((roff // 4).astype(np.int64)).to(dev)] = crc_d
+    return Encoded(out[:total], roff, flags, vsz.astype(np.uint32), crc)
+
+
+def _copy(src: torch.Tensor, src_off, length, dst: torch.Tensor, dst_off, stream=None):
+    L = _lib.lib()
+    n = len(src_off)
+    if n == 0:
+        return
+    dev = dst.device
+    so, ln, do = _dev_u64(src_off, dev), _dev_u32(length, dev), _dev_u64(dst_off, dev)
+    _lib.check(L.qlzx_copy_batch(src.data_ptr(), so.data_ptr(), ln.data_ptr(), dst.data_ptr(), do.data_ptr(), n,
+                                 batch._stream(stream)), "qlzx_copy_batch")
+
+
+def _gather_prefix(values: batch.BlockBatch, idx: np.ndarray, k: int) -> list[bytes]:
+    dev = values.data.device
+    off = values.off[torch.from_numpy(idx).to(dev)]
+    ln = values.length[torch.from_numpy(idx).to(dev)].to(torch.int64)
+    ar = torch.arange(k, device=dev)
+    pos = off.unsqueeze(1) + ar.unsqueeze(0)
+    pos = torch.minimum(pos, torch.tensor(values.data.numel() - 1, device=dev))
+    h = values.data[pos.reshape(-1)].reshape(len(idx), k).cpu().numpy()
+    lh = np.minimum(ln.cpu().numpy(), k)
+    return [h[j, : lh[j]].tobytes() for j in range(len(idx))]

@@ -135,6 +135,18 @@ int qlzx_synth_batch(int kind, uint64_t seed, uint64_t first_id, uint8_t *dst,
                      const uint8_t *vocab, const uint32_t *vocab_off, const uint32_t *zipf_cdf,
                      uint32_t nwords, void *stream);
 
+/* ---- write-side record encode ----
+ * Record CRC = ~crc_write(~0, header[4:24] ‖ key ‖ value) (store/datafile.go:66-88).
+ * qlzx_compress_batch fuses the value's raw CRC (crc_state = 0, crc_out = ~raw);
+ * this folds the header+key prefix in afterwards:
+ *   out[i] = (raw_a[i] * x^(8 len_b[i]) ^ raw_b[i]) ^ final_xor
+ * i.e. the raw state of A ‖ B from the raw state of A and the raw CRC (from 0) of B. */
+int qlzx_crc32_combine(const uint32_t *raw_a, const uint32_t *raw_b, const uint32_t *len_b, uint32_t n,
+                       uint32_t final_xor, uint32_t *out, void *stream);
+/* dst[dst_off[i] ..+ len[i]) = src[src_off[i] ..+ len[i]) (record assembly, WriteRecord.append). */
+int qlzx_copy_batch(const uint8_t *src, const uint64_t *src_off, const uint32_t *len, uint8_t *dst,
+                    const uint64_t *dst_off, uint32_t n, void *stream);
+
 /* ---- .data chunk replay ----
  * Replaces the DataStreamReader.Next loop of buildHintFromData
  * (store/datafile.go:202-277, store/bucket.go:89-117) over one chunk file that

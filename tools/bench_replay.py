@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Config c4: replay a synthetic .data corpus on one GPU, device-only and end-to-end.
+
+A chunk file (store/datafile.go layout: 24-B header, key, value, 256-B padding)
+of --chunk-mib MiB is built once from synthetic values (log-uniform 4-64 KiB,
+70 % text / 30 % image-like).  Values pass a simplified TryCompress policy
+(store/item.go:145: keep the compressed body when float32(clen)/float32(len) <= 0.7;
+the 10 KiB trial and the MIME sniff are not modelled here).  Keys are "key_%016x".
+--files copies of that chunk (13 x 4000 MiB ~ 50 GiB by default) are replayed:
+
+  device-only   the chunk is resident in HBM; one step = qlzx_replay_index +
+                decompress of FLAG_COMPRESS values + Getvhash (gobeansdb_amd.replay)
+  end-to-end    per file: pinned H2D of the chunk, the same replay, D2H of the
+                values (decompressed or raw) into pinned host memory
+
+Prints one JSON line.  The reference's sequential DataStreamReader is the CPU
+baseline for this path only in DESIGN.md prose (it is not shipped to the box).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import struct
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def log(*a):
+    print("[replay]", *a, file=sys.stderr, flush=True)
+
+
+def build_chunk(mib: int, seed: int, dev):
+    from gobeansdb_amd import batch
+    rng = np.random.default_rng(seed)
+    target = mib << 20
+    sizes, total = [], 0
+    while True:   # raw sizes for ~1.7x the target; records are cut at the target after compression
+        n = int(np.exp(rng.uniform(np.log(4096), np.log(65536))))
+        rs = (24 + 20 + n + 255) // 256 * 256
+        if total + rs > 1.7 * target:
+            break
+        sizes.append(n)
+        total += rs
+    nrec = len(sizes)
+    kinds = rng.random(nrec) < 0.7
+    log(f"chunk: {nrec} records, raw values {sum(sizes) / 2**30:.2f} GiB")
+    values = [None] * nrec
+    flags = np.zeros(nrec, np.uint32)
+    step = 8192
+    t0 = time.time()
+    for kind, mask in (("text", kinds), ("image", ~kinds)):
+        idx = np.nonzero(mask)[0]
+        for c0 in range(0, len(idx), step):
+            ids = idx[c0:c0 + step]
+            ln = [sizes[i] for i in ids]
+            plain = batch.synth(kind, seed, ln, first_id=int(ids[0]) * 7919, device=dev)
+            comp, cs, st, _ = batch.compress(plain, max_len=max(ln))
+            torch.cuda.synchronize()
+            ph = plain.to_bytes()
+            ch = comp.to_bytes(cs)
+            for j, i in enumerate(ids):
+                # TryCompress keep rule (store/item.go:145), float32 ratio
+                if np.float32(len(ch[j])) / np.float32(len(ph[j])) <= np.float32(0.7):
+                    values[i], flags[i] = ch[j], 0x10000
+                else:
+                    values[i] = ph[j]
+    log(f"values generated+compressed in {time.time() - t0:.1f}s, "
+        f"{int((flags != 0).sum())} compressed")
+    buf = np.zeros(target, np.uint8)
+    off = 0
+    crc_off, crc_len, rec_off = [], [], []
+    for i in range(nrec):
+        key = b"key_%016x" % (seed * 1000003 + i)
+        v = values[i]
+        hdr = struct.pack("<IIIiII", 0, 1700000000 + i, int(flags[i]), i % 7, len(key), len(v))
+        rec = hdr + key + v
+        if off + len(rec) > target:   # the chunk file is full (DataFileMax, store/config_default.go:39)
+            nrec = i
+            break
+        buf[off: off + len(rec)] = np.frombuffer(rec, np.uint8)
+        rec_off.append(off)
+        crc_off.append(off + 4)
+        crc_len.append(20 + len(key) + len(v))
+        off += (len(rec) + 255) // 256 * 256
+    buf = buf[:off]   # compressed values made the file shorter than the raw-size bound
+    # record CRCs (store/datafile.go:66-76) on the GPU, patched into the headers
+    from gobeansdb_amd import batch as B
+    d = torch.from_numpy(buf).to(dev)
+    crc = B.crc32(B.BlockBatch(d, torch.tensor(crc_off, dtype=torch.int64, device=dev),
+                               torch.tensor(crc_len, dtype=torch.int32, device=dev)))
+    c = crc.cpu().numpy().view(np.uint32)
+    for o, v in zip(rec_off, c):
+        buf[o: o + 4] = np.frombuffer(struct.pack("<I", int(v)), np.uint8)
+    del d
+    return buf, nrec, int(sum(len(v) for v in values[:nrec])), int(sum(sizes[:nrec]))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--chunk-mib", type=int, default=4000)
+    p.add_argument("--files", type=int, default=13)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--seed", type=int, default=2026)
+    a = p.parse_args()
+    from gobeansdb_amd import replay, batch
+    dev = torch.device("cuda", 0)
+    t0 = time.time()
+    host, nrec, stored_bytes, raw_bytes = build_chunk(a.chunk_mib, a.seed, dev)
+    log(f"chunk built in {time.time() - t0:.1f}s: {len(host) / 2**20:.0f} MiB, {nrec} records")
+    pinned = torch.from_numpy(host).pin_memory()
+    dchunk = pinned.to(dev, non_blocking=False)
+    ws = batch.Workspace(dev)
+    # correctness gate: every record found, no resync, values decompressed to their raw sizes
+    res = replay.replay(dchunk, workspace=ws)
+    torch.cuda.synchronize()
+    assert res.n == nrec and not res.end_error, (res.n, nrec, res.end_error)
+    assert int(res.size_broken.abs().sum()) == 0
+    assert int(res.value_len.to(torch.int64).sum()) == raw_bytes, "decompressed sizes"
+    assert int(((res.flag & 0x10000) != 0).sum()) == 0, "a compressed value failed to decode"
+    log("replay verified: all records, all values decoded")
+
+    # ---- device-only ----
+    for _ in range(1):
+        replay.replay(dchunk, workspace=ws)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(a.steps):
+        replay.replay(dchunk, workspace=ws)
+    torch.cuda.synchronize()
+    dev_s = (time.perf_counter() - t) / a.steps
+
+    # ---- end-to-end: H2D chunk, replay, D2H values ----
+    # only decompressed values travel back: raw values are bytes the host already holds (its own file)
+    out_host = torch.empty(max(res.values.data.numel(), 1), dtype=torch.uint8).pin_memory()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(a.files):
+        dchunk.copy_(pinned, non_blocking=True)
+        r = replay.replay(dchunk, workspace=ws)
+        out_host[: r.values.data.numel()].copy_(r.values.data, non_blocking=True)
+    torch.cuda.synchronize()
+    e2e_s = time.perf_counter() - t
+    chunk_gib = len(host) / 2**30
+    rec = {
+        "metric": "GiB/s .data replay (record scan + CRC + decompress + vhash), c4",
+        "chunk_mib": a.chunk_mib, "records_per_chunk": nrec,
+        "compressed_values": int(((res.header[:, 2] & 0x10000) != 0).sum()),
+        "device_only": {"gib_per_s_chunk": round(chunk_gib / dev_s, 2),
+                        "gib_per_s_values_out": round(raw_bytes / 2**30 / dev_s, 2),
+                        "ms_per_chunk": round(dev_s * 1e3, 2)},
+        "end_to_end": {"files": a.files, "total_gib": round(chunk_gib * a.files, 2),
+                       "gib_per_s_chunk": round(chunk_gib * a.files / e2e_s, 2),
+                       "seconds": round(e2e_s, 2),
+                       "note": "sequential per file: pinned H2D of the chunk, replay, pinned D2H of the decompressed values"},
+        "data": "synthetic",
+    }
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
