@@ -256,7 +256,11 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
 // mem = (mem & ~mask) | val in one LDS instruction (val pre-masked).
 __device__ __forceinline__ void lds_mskor(uint32_t *addr, uint32_t mask, uint32_t val) {
     const uint32_t a = (uint32_t)(uintptr_t)addr;
+#ifdef QLZX_EXP_PLAINWRITE  // experiment: plain dword stores (wrong bytes; timing only)
+    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(val | mask) : "memory");
+#else
     asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(a), "v"(mask), "v"(val) : "memory");
+#endif
 }
 
 template <uint32_t MAXD>
@@ -522,9 +526,8 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
                             out[d + j] = out[s + j2];
                             j2 = (j2 + 1 == off) ? 0 : j2 + 1;
                         }
-                    } else {  // 16-B chunks, in order when the source overlaps the destination
+                    } else {  // 16-B chunks, in issue order (so an overlapping source sees earlier chunks)
                         for (uint32_t c = 0; c < len; c += 16) {
-                            if (c && off < len) lds_sync();
                             Copy16 c2;
                             c2.prep(d + c, off, len - c < 16 ? len - c : 16);
                             c2.run(out);
@@ -533,7 +536,8 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
                 }
             }
             done = done || ready;
-            lds_sync();
+            // no lgkmcnt wait: a wave's LDS operations execute in issue order, so the
+            // next sub-round's reads observe these writes
             pend = __ballot(!done);
         }
         PROF_MARK(3);  // 3: match sub-rounds
@@ -608,8 +612,11 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
             hipLaunchKernelGGL(k_dec_parse<false>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s, b,
                                dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax);
         if (md <= 16384) {
-            hipLaunchKernelGGL(k_dec_blocks<16384>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
-                               recs, gmax, (const uint32_t *)nullptr);
+#ifndef QLZX_EXP_K2_EXTRA_LDS
+#define QLZX_EXP_K2_EXTRA_LDS 0  // experiments: extra dynamic LDS per WG to lower occupancy
+#endif
+            hipLaunchKernelGGL(k_dec_blocks<16384>, dim3(cnt), dim3(64), QLZX_EXP_K2_EXTRA_LDS, s, b, dsize, status,
+                               first, cnt, info, recs, gmax, (const uint32_t *)nullptr);
         } else {
             // mixed sizes: route every block to the smallest K2 whose LDS history holds it
             hipError_t e = hipMemsetAsync(cls_counts, 0, kClasses * sizeof(uint32_t), s);

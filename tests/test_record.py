@@ -59,7 +59,7 @@ def test_encode_policy_edges(cuda):
     vers = [1, 1, 1, 1, 1, -1]
     keys = [b"k%d" % i for i in range(len(vals))]
     enc = record.encode(keys, batch.BlockBatch.from_bytes(vals), flags=flags, vers=vers)
-    exp = b""
+    exp, exp_flags = b"", []
     for k, v, f, ver in zip(keys, vals, flags, vers):
         body, fl = v, f
         if ver >= 0 and (24 + len(k) + len(v) + 255) // 256 * 256 > 256 and not v.startswith(b"ID3"):
@@ -68,5 +68,7 @@ def test_encode_policy_edges(cuda):
             if np.float32(len(c)) / np.float32(len(t)) <= np.float32(0.7):
                 body, fl = (O.compress(v) if len(v) > len(t) else c), f | 0x10000
         exp += R.make_record(k, body, flag=fl, ver=ver)
+        exp_flags.append(fl)
     assert enc.data.cpu().numpy().tobytes() == exp
-    assert [int(f) & 0x10000 for f in enc.flag] == [0, 0x10000, 0x10000, 0, 0, 0]
+    assert [int(f) for f in enc.flag] == exp_flags
+    assert exp_flags[1] == 0x10000 and exp_flags[0] == exp_flags[3] == exp_flags[4] == exp_flags[5] == 0
