@@ -52,6 +52,10 @@ constexpr uint32_t kChunkBlocks = 131072;  // >= 256 CUs x 8 waves x 64 lanes: K
 constexpr uint32_t kRoundBytes = 64;          // bytes DMA'd per lane per round (4 x 16 B)
 constexpr uint32_t kRingSlots = 4;            // rounds resident per lane: r-1..r (read), r+1..r+2 (landing)
 constexpr uint32_t kRingWave = kRingSlots * kRoundBytes * 64;  // 16 KiB per wave
+#ifndef QLZX_K2_WIN
+#define QLZX_K2_WIN 4096
+#endif
+constexpr uint32_t kWin = QLZX_K2_WIN;          // K2 LDS history window (bytes)
 constexpr uint32_t kK2Slack = 3;              // K2: iterations a prefetch DMA has to land
 constexpr uint32_t kTokAhead = kK2Slack + 1;   // tokens of batch bt + 4 issued in iteration bt
 constexpr uint32_t kRecAhead = 2 * kTokAhead;  // records of batch bt + 8 issued in iteration bt
@@ -69,8 +73,7 @@ inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
     const uint32_t md = max_dsize > QLZX_FAST_MAX_DSIZE ? QLZX_FAST_MAX_DSIZE : max_dsize;
     const uint32_t c = n < kChunkBlocks ? (n ? n : 1) : kChunkBlocks;
     return (((size_t)c * sizeof(BlkInfo) + 255) & ~(size_t)255) +
-           ((((size_t)c * groups_max(md) * sizeof(GroupRec)) + 255) & ~(size_t)255) +
-           (((size_t)3 * c * sizeof(uint32_t) + 255) & ~(size_t)255) + 256;
+           ((((size_t)c * groups_max(md) * sizeof(GroupRec)) + 255) & ~(size_t)255) + 256;
 }
 
 // ------------------------------------------------------------------ K1 ----
@@ -263,11 +266,15 @@ __device__ __forceinline__ void lds_mskor(uint32_t *addr, uint32_t mask, uint32_
 #endif
 }
 
-template <uint32_t MAXD>
+// K2 shared memory: prefetch slots, then the output window.  Output position
+// p lives at win[p - base] for p in [base, base + W); older output has been
+// flushed to the block's destination in HBM ("window").
+template <uint32_t W>
 struct K2Lds {
     GroupRec rec[kRecSlots][4];      // records of the <= 4 groups of batches bt+4..bt+8
     uint32_t tok[kTokSlots][64];     // per-lane token dword of batches bt..bt+3
-    uint8_t out[MAXD + 16];          // a match's first source dword may start 4 B before out[0] (reads tok)
+    uint8_t win[W + 32];             // a source dword may start 4 B before win[0] (reads tok);
+                                     // reads run <= 24 B past a write; win[W + 24] = literal dummy
 };
 
 // Every K2 iteration issues exactly 2 DMA instructions (1 token dword + 1
@@ -350,6 +357,22 @@ struct Copy16 {
         }
         mk[0] &= 0xffffffffu << (8 * lo);
     }
+    // as run(), but lanes with `far` set take their source dwords from y[] (HBM)
+    __device__ __forceinline__ void run_sel(uint8_t *out, bool far, const uint32_t y[5]) const {
+        const uint32_t *x = (const uint32_t *)(out + (far ? 0 : xa));
+        const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4], x5 = x[5];
+        const uint32_t v0 = far ? y[0] : __builtin_amdgcn_alignbyte(x1, x0, sh);
+        const uint32_t v1 = far ? y[1] : __builtin_amdgcn_alignbyte(x2, x1, sh);
+        const uint32_t v2 = far ? y[2] : __builtin_amdgcn_alignbyte(x3, x2, sh);
+        const uint32_t v3 = far ? y[3] : __builtin_amdgcn_alignbyte(x4, x3, sh);
+        const uint32_t v4 = far ? y[4] : __builtin_amdgcn_alignbyte(x5, x4, sh);
+        uint32_t *dw = (uint32_t *)(out + qa);
+        lds_mskor(dw + 0, mk[0], v0 & mk[0]);
+        lds_mskor(dw + 1, mk[1], v1 & mk[1]);
+        lds_mskor(dw + 2, mk[2], v2 & mk[2]);
+        lds_mskor(dw + 3, mk[3], v3 & mk[3]);
+        lds_mskor(dw + 4, mk[4], v4 & mk[4]);
+    }
     __device__ __forceinline__ void run(uint8_t *out) const {
         const uint32_t *x = (const uint32_t *)(out + xa);
         const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4], x5 = x[5];
@@ -377,11 +400,34 @@ __device__ __forceinline__ uint32_t ff1_or(uint64_t m, uint32_t dflt) {
     return m ? (uint32_t)__builtin_ctzll(m) : dflt;
 }
 
-template <uint32_t MAXD>
-__global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
+// Far source (below the window): 20 bytes from HBM starting at s - lo, as the five
+// destination-aligned dwords y[j] = bytes [s - lo + 4j, s - lo + 4j + 4) (the lo
+// leading bytes are masked off by the caller).  Loads are clamped inside [0, lim).
+__device__ __forceinline__ void far_load20(const uint8_t *dst, uint32_t s, uint32_t lo, uint32_t lim,
+                                           uint32_t y[5]) {
+    uint32_t x[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        uint32_t a = s + 4 * j;
+        a = a + 4 <= lim ? a : lim - 4;
+        x[j] = *(const uint32_t *)(dst + a);  // unaligned dword load (unaligned access mode)
+    }
+    const uint32_t sh = (4 - lo) & 3;
+    y[0] = lo ? __builtin_amdgcn_alignbyte(x[0], 0u, sh) : x[0];
+#pragma unroll
+    for (int j = 1; j < 5; j++) y[j] = lo ? __builtin_amdgcn_alignbyte(x[j], x[j - 1], sh) : x[j];
+}
+
+#ifndef QLZX_K2_WAVES_PER_EU
+#define QLZX_K2_WAVES_PER_EU 1
+#endif
+template <uint32_t W>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLZX_K2_WAVES_PER_EU)))
+k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                                                    uint32_t first, uint32_t count, const BlkInfo *info,
                                                    const GroupRec *recs, uint32_t gmax, const uint32_t *list) {
-    __shared__ __attribute__((aligned(16))) K2Lds<MAXD> L;
+    static_assert(W % 2048 == 0 && W >= 2048, "window: a multiple of 2 KiB (slides by W/2)");
+    __shared__ __attribute__((aligned(16))) K2Lds<W> L;
     const uint32_t lane = threadIdx.x;
     if (blockIdx.x >= count) return;
     const uint32_t li = list ? list[blockIdx.x] : blockIdx.x;  // block of the chunk (size-class list)
@@ -397,13 +443,14 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
         if (lane == 0) { status[i] = QLZX_OK; if (dsize_out) dsize_out[i] = dsize; }
         return;
     }
-    uint8_t *out = L.out;
+    uint8_t *win = L.win;
     const GroupRec *rb = recs + (size_t)li * gmax;
     const uint32_t nitems = bi.nitems, ngroups = bi.ngroups;
     const uint32_t csize = b.src_len[i];
     const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
     const uint32_t nb = (nitems + 63) / 64;
     const uint32_t tail_from = dsize > QLZX_TAIL ? dsize - 1 - QLZX_TAIL : 0;  // op >= this: tail (quicklz.c:503)
+    const bool a16 = (((uintptr_t)dst) & 15u) == 0;
 
     // prologue: records of batches 0..3, the tokens of batches 0..3 (which read
     // those records), then the records of batches 4..7 (slots 4, 0, 1, 2)
@@ -411,25 +458,17 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
     vm_sync();
     ItemCursor cur{lane / 31, lane % 31};  // item coordinates of the next batch to issue
     uint32_t pm[kTokAhead];
-#ifdef QLZX_K2_REGTOK
-    uint32_t twr[kTokAhead];
-#endif
 #pragma unroll
     for (uint32_t j = 0; j < kTokAhead; j++) {
         const bool v = j * 64 + lane < nitems;
-#ifdef QLZX_K2_REGTOK
-        uint32_t pj;
-        pm[j] = issue_tok<false>(tok_rec(L.rec[j], (j * 64) / 31, cur, v), cur, v, L.tok[j], src, csize, &pj);
-        twr[j] = *(const uint32_t *)(src + pj);
-#else
         pm[j] = issue_tok(tok_rec(L.rec[j], (j * 64) / 31, cur, v), cur, v, L.tok[j], src, csize);
-#endif
         cur.next();
     }
     for (uint32_t j = kTokAhead; j < kRecAhead; j++) issue_rec(L.rec[j % kRecSlots], rb, (j * 64) / 31, ngroups, lane);
     vm_sync();
     PROF_DECL
-    uint32_t D = 0;                   // output bytes of all earlier batches
+    uint32_t D = 0;                   // output bytes of all earlier items
+    uint32_t base = 0;                // window start (multiple of W/2)
     bool err = false;                 // per-lane: a check failed on this lane's item
     bool tail = false, complete = dsize == 0;
     // slot counters: tokens of bt (read) and bt+4 (issue); records of bt+4 (read) and bt+8 (issue)
@@ -437,35 +476,16 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
     for (uint32_t bt = 0; bt < nb && !complete; bt++) {
         // this batch's token dword, and the record the prefetch of batch bt+4 needs;
         // both reads complete before that prefetch reuses this batch's token slot
-#ifdef QLZX_K2_REGTOK
-        const uint32_t tw = twr[0];
-#pragma unroll
-        for (uint32_t j = 0; j + 1 < kTokAhead; j++) twr[j] = twr[j + 1];
-#else
         const uint32_t tw = L.tok[ts][lane];
-#endif
         const bool v4 = (bt + kTokAhead) * 64 + lane < nitems;
         const GroupRec gr4 = tok_rec(L.rec[rs4], ((bt + kTokAhead) * 64) / 31, cur, v4);
         lds_sync();
         const uint32_t posm = pm[0];
 #pragma unroll
         for (uint32_t j = 0; j + 1 < kTokAhead; j++) pm[j] = pm[j + 1];
-#ifdef QLZX_EXP_NODMA  // experiment: no loop prefetch (wrong output; timing only)
-        constexpr bool kLoopDma = false;
-#else
-        constexpr bool kLoopDma = true;
-#endif
-#ifdef QLZX_K2_REGTOK
-        {
-            uint32_t p4;
-            pm[kTokAhead - 1] = issue_tok<false>(gr4, cur, v4, L.tok[ts], src, csize, &p4);
-            twr[kTokAhead - 1] = *(const uint32_t *)(src + p4);
-        }
-#else
-        pm[kTokAhead - 1] = issue_tok<kLoopDma>(gr4, cur, v4, L.tok[ts], src, csize);
-#endif
+        pm[kTokAhead - 1] = issue_tok(gr4, cur, v4, L.tok[ts], src, csize);
         cur.next();
-        issue_rec<kLoopDma>(L.rec[rs8], rb, ((bt + kRecAhead) * 64) / 31, ngroups, lane);
+        issue_rec(L.rec[rs8], rb, ((bt + kRecAhead) * 64) / 31, ngroups, lane);
         ts = ts == kTokSlots - 1 ? 0 : ts + 1;
         rs4 = rs4 == kRecSlots - 1 ? 0 : rs4 + 1;
         rs8 = rs8 == kRecSlots - 1 ? 0 : rs8 + 1;
@@ -476,74 +496,108 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
         const uint32_t t = pos + 4 <= csize ? tw : tw >> (8 * (pos + 4 - csize));
         uint32_t off, mlen, tl;
         decode_tok_bf(t, off, mlen, tl);
-        const uint32_t len = ism ? mlen : (valid ? 1u : 0u);
+        const uint32_t len0 = ism ? mlen : (valid ? 1u : 0u);
         tl = ism ? tl : 1u;
-        const uint32_t incl = wave_incl_scan(len);
-        const uint32_t d = D + incl - len;
-        D += __builtin_amdgcn_readlane(incl, 63);
-        // ---- checks C2-C5 on the live items (those that start before dsize) ----
-        const bool live = valid && d < dsize;
-        const uint64_t tail_lanes = __ballot(live && !ism && d >= tail_from);
-        const uint32_t tail_lane = tail ? 0u : ff1_or(tail_lanes, 64u);  // C4: no match after it
-        tail = tail || tail_lanes != 0;
-        const bool mok = off >= 3 && off <= d && d + len + 4 <= dsize && lane < tail_lane;  // C3, C4
-        const bool last = live && d + len == dsize;  // C5: the item completing dsize ends the stream
-        const uint32_t ip_end = pos + tl;
-        const bool eok = ip_end == csize || (ip_end < hdr + 9 && csize == hdr + 9);
-        const bool bad = live && ((ism && !mok) || (last && !eok));
-        err = err || bad;
-        complete = __ballot(last) != 0;
-        PROF_MARK(2);  // 2: decode + scan + checks
-        // literals (non-literal lanes store to an unused byte past MAXD)
-        out[(live && !ism) ? d : MAXD + 8] = (uint8_t)t;
-        // ---- matches: copy in sub-rounds ----
-        bool done = !(live && ism && !bad);
-        const uint32_t s = d - off;
-        const uint32_t send = (s + len < d) ? s + len : d;
-        const uint32_t end = d + len;
-        const bool spec = off < len || len > 16;  // overlapping or long: byte / chunked path
-        Copy16 cp;
-        cp.prep(d, off, len < 16 ? len : 16);
-        uint64_t pend = __ballot(!done);
-        while (pend) {
-            // the first three pending matches bound three gaps whose bytes are all final
-            const uint32_t u0 = (uint32_t)__builtin_ctzll(pend);
-            const uint64_t p1 = pend & (pend - 1), p2 = p1 & (p1 - 1);
-            const uint32_t u1 = ff1_or(p1, u0), u2 = ff1_or(p2, u0);
-            const uint32_t d0 = __builtin_amdgcn_readlane(d, u0), e0 = __builtin_amdgcn_readlane(end, u0);
-            const uint32_t d1r = __builtin_amdgcn_readlane(d, u1), e1 = __builtin_amdgcn_readlane(end, u1);
-            const uint32_t d2r = __builtin_amdgcn_readlane(d, u2);
-            const uint32_t d1 = p1 ? d1r : 0xffffffffu, d2 = p2 ? d2r : 0xffffffffu;
-            const bool ready = !done & ((send <= d0) | ((s >= e0) & (send <= d1)) | ((s >= e1) & (send <= d2)));
-#ifndef QLZX_EXP_NOCOPY
-            if (ready && !spec) cp.run(out);
-#endif
-            if (__ballot(ready && spec)) {
-                if (ready && spec) {
-                    if (off < 16 && off < len) {  // short-period overlap: byte by byte
-                        uint32_t j2 = 0;
-                        for (uint32_t j = 0; j < len; j++) {
-                            out[d + j] = out[s + j2];
-                            j2 = (j2 + 1 == off) ? 0 : j2 + 1;
-                        }
-                    } else {  // 16-B chunks, in issue order (so an overlapping source sees earlier chunks)
-                        for (uint32_t c = 0; c < len; c += 16) {
-                            Copy16 c2;
-                            c2.prep(d + c, off, len - c < 16 ? len - c : 16);
-                            c2.run(out);
+        // ---- sub-batches: normally one; more when the batch's output overflows the window ----
+        uint32_t lo_lane = 0;
+        bool more = true;
+        while (more) {
+            const bool act = lane >= lo_lane;
+            const uint32_t len = act ? len0 : 0u;
+            uint32_t incl = wave_incl_scan(len);
+            uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+            if (D + total > base + W && D - base >= W / 2) {
+                // slide: flush win[0, W/2) to HBM, move the rest down, base += W/2
+                for (uint32_t q = lane * 16; q < W / 2; q += 1024) {
+                    const uint4 v = *(const uint4 *)(win + q);
+                    if (a16) *(uint4 *)(dst + base + q) = v;
+                    else for (uint32_t k = 0; k < 16; k++) dst[base + q + k] = win[q + k];
+                }
+                for (uint32_t q = lane * 16; q < D - base - W / 2; q += 1024)
+                    *(uint4 *)(win + q) = *(const uint4 *)(win + W / 2 + q);
+                base += W / 2;
+            }
+            const uint32_t d = D + incl - len;
+            // this sub-batch: the active lanes whose output fits the window (a prefix)
+            const bool fits = d + len <= base + W;
+            const uint64_t outm = __ballot(act && len && !fits);
+            const uint32_t cut = outm ? (uint32_t)__builtin_ctzll(outm) : 64u;
+            const bool in = act && lane < cut;
+            more = cut < 64;
+            lo_lane = cut;
+            const uint32_t stotal = cut < 64 ? __builtin_amdgcn_readlane(incl - len, cut) : total;
+            // far sources (below the window, already in HBM): load them first, use them in the first sub-round
+            const uint32_t s = d - off;
+            const bool far = s < base;
+            const bool spec = off < len || len > 16 || (far && s + len > base);  // byte / chunked path
+            uint32_t fy[5] = {0, 0, 0, 0, 0};
+            const bool fload = in && valid && ism && far && !spec;
+            if (__ballot(fload)) {
+                if (fload) far_load20(dst, s, d & 3u, dsize, fy);
+            }
+            // ---- checks C2-C5 on the live items (those that start before dsize) ----
+            const bool live = in && valid && d < dsize;
+            const uint64_t tail_lanes = __ballot(live && !ism && d >= tail_from);
+            const uint32_t tail_lane = tail ? 0u : ff1_or(tail_lanes, 64u);  // C4: no match after it
+            tail = tail || tail_lanes != 0;
+            const bool mok = off >= 3 && off <= d && d + len + 4 <= dsize && lane < tail_lane;  // C3, C4
+            const bool last = live && d + len == dsize;  // C5: the item completing dsize ends the stream
+            const uint32_t ip_end = pos + tl;
+            const bool eok = ip_end == csize || (ip_end < hdr + 9 && csize == hdr + 9);
+            const bool bad = live && ((ism && !mok) || (last && !eok));
+            err = err || bad;
+            complete = __ballot(last) != 0;
+            if (complete) more = false;
+            PROF_MARK(2);  // 2: decode + scan + checks
+            // literals (non-literal lanes store to an unused byte past the window)
+            win[(live && !ism) ? d - base : W + 24] = (uint8_t)t;
+            // ---- matches: copy in sub-rounds ----
+            bool done = !(live && ism && !bad);
+            const uint32_t send = (s + len < d) ? s + len : d;
+            const uint32_t end = d + len;
+            const uint32_t n16 = len < 16 ? len : 16;
+            Copy16 cp;
+            cp.prep(d - base, off, n16);
+            uint64_t pend = __ballot(!done);
+            while (pend) {
+                // the first three pending matches bound three gaps whose bytes are all final
+                const uint32_t u0 = (uint32_t)__builtin_ctzll(pend);
+                const uint64_t p1 = pend & (pend - 1), p2 = p1 & (p1 - 1);
+                const uint32_t u1 = ff1_or(p1, u0), u2 = ff1_or(p2, u0);
+                const uint32_t d0 = __builtin_amdgcn_readlane(d, u0), e0 = __builtin_amdgcn_readlane(end, u0);
+                const uint32_t d1r = __builtin_amdgcn_readlane(d, u1), e1 = __builtin_amdgcn_readlane(end, u1);
+                const uint32_t d2r = __builtin_amdgcn_readlane(d, u2);
+                const uint32_t d1 = p1 ? d1r : 0xffffffffu, d2 = p2 ? d2r : 0xffffffffu;
+                const bool ready = !done & ((send <= d0) | ((s >= e0) & (send <= d1)) | ((s >= e1) & (send <= d2)));
+                if (ready && !spec) cp.run_sel(win, far, fy);
+                if (__ballot(ready && spec)) {
+                    if (ready && spec) {
+                        if (far || (off < 16 && off < len)) {
+                            // byte by byte, in order (short-period overlap, or a source in HBM)
+                            for (uint32_t j = 0; j < len; j++) {
+                                const uint32_t sp = s + j;  // = d + j - off: earlier bytes of this copy included
+                                const uint8_t v = sp < base ? dst[sp] : win[sp - base];
+                                win[d + j - base] = v;
+                            }
+                        } else {  // 16-B chunks, in issue order (so an overlapping source sees earlier chunks)
+                            for (uint32_t c = 0; c < len; c += 16) {
+                                Copy16 c2;
+                                c2.prep(d + c - base, off, len - c < 16 ? len - c : 16);
+                                c2.run(win);
+                            }
                         }
                     }
                 }
+                done = done || ready;
+                // no lgkmcnt wait: a wave's LDS operations execute in issue order, so the
+                // next sub-round's reads observe these writes
+                pend = __ballot(!done);
             }
-            done = done || ready;
-            // no lgkmcnt wait: a wave's LDS operations execute in issue order, so the
-            // next sub-round's reads observe these writes
-            pend = __ballot(!done);
+            PROF_MARK(3);  // 3: match sub-rounds
+            D += stotal;
+            if (__ballot(err)) { more = false; complete = false; }
         }
-        PROF_MARK(3);  // 3: match sub-rounds
-#ifndef QLZX_EXP_NOBREAK
         if (__ballot(err)) break;
-#endif
         asm volatile("s_waitcnt vmcnt(" QLZX_STR(QLZX_K2_VMWAIT) ")" ::: "memory");  // DMAs of iterations <= bt-3 landed
         PROF_MARK(4);  // 4: waiting for prefetch
     }
@@ -554,14 +608,13 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
         if (lane == 0) { status[i] = QLZX_E_CORRUPT; if (dsize_out) dsize_out[i] = 0; }
         return;
     }
-    // write the block out: 16 B per lane, 1 KiB per wave instruction
-    const bool a16 = (((uintptr_t)dst) & 15u) == 0;
-    for (uint32_t p = lane * 16; p < dsize; p += 1024) {
+    // write the rest of the block out: 16 B per lane, 1 KiB per wave instruction
+    for (uint32_t p = base + lane * 16; p < dsize; p += 1024) {
         if (p + 16 <= dsize && a16) {
-            *(uint4 *)(dst + p) = *(const uint4 *)(out + p);
+            *(uint4 *)(dst + p) = *(const uint4 *)(win + (p - base));
         } else {
             const uint32_t e = p + 16 < dsize ? p + 16 : dsize;
-            for (uint32_t q = p; q < e; q++) dst[q] = out[q];
+            for (uint32_t q = p; q < e; q++) dst[q] = win[q - base];
         }
     }
     PROF_MARK(5);  // 5: write-out (not flushed: stamps of the loop only)
@@ -569,18 +622,6 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
         status[i] = QLZX_OK;
         if (dsize_out) dsize_out[i] = dsize;
     }
-}
-
-// Size classes for mixed batches: K2<16384> (9 WGs/CU), K2<32768>, K2<65536>.
-constexpr uint32_t kClasses = 3;
-__global__ void __launch_bounds__(256) k_dec_classify(const BlkInfo *info, uint32_t count, uint32_t *lists,
-                                                      uint32_t *counts) {
-    const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
-    if (li >= count) return;
-    const BlkInfo bi = info[li];
-    if (bi.kind == kBlkSkip) return;
-    const uint32_t c = bi.dsize <= 16384 ? 0u : (bi.dsize <= 32768 ? 1u : 2u);
-    lists[(size_t)c * count + atomicAdd(&counts[c], 1u)] = li;
 }
 
 inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uint32_t *dsize,
@@ -594,14 +635,6 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     BlkInfo *info = (BlkInfo *)ws;
     const size_t o_rec = ((size_t)chunk * sizeof(BlkInfo) + 255) & ~(size_t)255;
     GroupRec *recs = (GroupRec *)((uint8_t *)ws + o_rec);
-    const size_t o_lists = o_rec + ((((size_t)chunk * gmax * sizeof(GroupRec)) + 255) & ~(size_t)255);
-    uint32_t *cls_lists = (uint32_t *)((uint8_t *)ws + o_lists);
-    uint32_t *cls_counts = (uint32_t *)((uint8_t *)ws + o_lists + ((((size_t)3 * chunk * 4) + 255) & ~(size_t)255));
-    static thread_local uint32_t *h_counts = nullptr;  // pinned, for the class counts
-    if (md > 16384 && !h_counts) {
-        hipError_t e = hipHostMalloc((void **)&h_counts, 64, hipHostMallocDefault);
-        if (e != hipSuccess) return (int)e;
-    }
     const bool crc = crc_state || crc_expect || crc_out;
     for (uint32_t first = 0; first < b.n; first += chunk) {
         const uint32_t cnt = b.n - first < chunk ? b.n - first : chunk;
@@ -611,32 +644,12 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         else
             hipLaunchKernelGGL(k_dec_parse<false>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s, b,
                                dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax);
-        if (md <= 16384) {
 #ifndef QLZX_EXP_K2_EXTRA_LDS
 #define QLZX_EXP_K2_EXTRA_LDS 0  // experiments: extra dynamic LDS per WG to lower occupancy
 #endif
-            hipLaunchKernelGGL(k_dec_blocks<16384>, dim3(cnt), dim3(64), QLZX_EXP_K2_EXTRA_LDS, s, b, dsize, status,
-                               first, cnt, info, recs, gmax, (const uint32_t *)nullptr);
-        } else {
-            // mixed sizes: route every block to the smallest K2 whose LDS history holds it
-            hipError_t e = hipMemsetAsync(cls_counts, 0, kClasses * sizeof(uint32_t), s);
-            if (e != hipSuccess) return (int)e;
-            hipLaunchKernelGGL(k_dec_classify, dim3((cnt + 255) / 256), dim3(256), 0, s, info, cnt, cls_lists,
-                               cls_counts);
-            e = hipMemcpyAsync(h_counts, cls_counts, kClasses * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e != hipSuccess) return (int)e;
-            if (h_counts[0])
-                hipLaunchKernelGGL(k_dec_blocks<16384>, dim3(h_counts[0]), dim3(64), 0, s, b, dsize, status, first,
-                                   h_counts[0], info, recs, gmax, (const uint32_t *)cls_lists);
-            if (h_counts[1])
-                hipLaunchKernelGGL(k_dec_blocks<32768>, dim3(h_counts[1]), dim3(64), 0, s, b, dsize, status, first,
-                                   h_counts[1], info, recs, gmax, (const uint32_t *)(cls_lists + cnt));
-            if (h_counts[2])
-                hipLaunchKernelGGL(k_dec_blocks<QLZX_FAST_MAX_DSIZE>, dim3(h_counts[2]), dim3(64), 0, s, b, dsize,
-                                   status, first, h_counts[2], info, recs, gmax,
-                                   (const uint32_t *)(cls_lists + 2 * (size_t)cnt));
-        }
+        // one kernel for every block size: the LDS window slides over longer blocks
+        hipLaunchKernelGGL(k_dec_blocks<kWin>, dim3(cnt), dim3(64), QLZX_EXP_K2_EXTRA_LDS, s, b, dsize, status,
+                           first, cnt, info, recs, gmax, (const uint32_t *)nullptr);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }

@@ -1,7 +1,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-for x in 0 2400 9500 22000; do
-  lib=gobeansdb_amd/libqlzx.so; [ $x -ne 0 ] && lib=gobeansdb_amd/libqlzx_occ$x.so
-  QLZX_LIB=$lib bash tools/prof.sh occ$x --blocks 262144 --unique 16384 --steps 3 --warmup 1 --no-cpu | grep "k_dec_blocks" | cut -c1-20,140-200 || exit 1
-done
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/r14_pytest.txt 2>&1; rc=$?
+tail -3 gpurun_out/r14_pytest.txt
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python tools/bench_replay.py --files 13 > gpurun_out/c4_r14.json 2> gpurun_out/c4_r14.err; rc=$?; tail -2 gpurun_out/c4_r14.err; cat gpurun_out/c4_r14.json; exit $rc
