@@ -49,9 +49,13 @@ constexpr int32_t kPending = -1;  // status of blocks left to the general path
 constexpr uint32_t kBlkSkip = 0, kBlkStored = 1, kBlkCompressed = 2;
 constexpr uint32_t kParseWG = 64;          // K1 workgroup: one wave (LDS per wave bounds occupancy)
 constexpr uint32_t kChunkBlocks = 131072;  // >= 256 CUs x 8 waves x 64 lanes: K1 fills the chip
-constexpr uint32_t kRoundBytes = 64;          // bytes DMA'd per lane per round (4 x 16 B)
+#ifndef QLZX_K1_ROUND
+#define QLZX_K1_ROUND 64
+#endif
+constexpr uint32_t kRoundBytes = QLZX_K1_ROUND;  // bytes DMA'd per lane per round (16 B pieces)
+constexpr uint32_t kPieces = kRoundBytes / 16;
 constexpr uint32_t kRingSlots = 4;            // rounds resident per lane: r-1..r (read), r+1..r+2 (landing)
-constexpr uint32_t kRingWave = kRingSlots * kRoundBytes * 64;  // 16 KiB per wave
+constexpr uint32_t kRingWave = kRingSlots * kRoundBytes * 64;  // 16 KiB per wave at 64-B rounds
 #ifndef QLZX_K2_WIN
 #define QLZX_K2_WIN 4096
 #endif
@@ -81,7 +85,7 @@ inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
 // (q = p + shift, shift = src & 15) lives in round q/64, slot (q/64) % 4,
 // piece (q/16) % 4, byte q % 16 -- i.e. at ((q/16) % 16) * 1 KiB + lane * 16 + q % 16.
 __device__ __forceinline__ uint32_t ring_off(uint32_t q, uint32_t lane) {
-    return (((q >> 4) & 15u) << 10) | (lane << 4) | (q & 15u);
+    return (((q >> 4) & (kPieces * kRingSlots - 1)) << 10) | (lane << 4) | (q & 15u);
 }
 __device__ __forceinline__ uint32_t ring_rd32(const uint8_t *ring, uint32_t q, uint32_t lane) {
     const uint32_t qa = q & ~3u;
@@ -97,10 +101,10 @@ __device__ __forceinline__ uint32_t ring_rd32(const uint8_t *ring, uint32_t q, u
 __device__ __forceinline__ void ring_issue(uint8_t *ring_wave, const uint8_t *gbase, const uint8_t *dummy,
                                            uint32_t r, uint32_t last16, bool active) {
 #pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-        const uint32_t c16 = r * 4 + j;
+    for (uint32_t j = 0; j < kPieces; j++) {
+        const uint32_t c16 = r * kPieces + j;
         const uint8_t *g = (active && c16 <= last16) ? gbase + (size_t)c16 * 16 : dummy;
-        dma16(g, lds_addr(ring_wave + ((r & (kRingSlots - 1)) * 4 + j) * 1024));
+        dma16(g, lds_addr(ring_wave + ((r & (kRingSlots - 1)) * kPieces + j) * 1024));
     }
 }
 
@@ -171,7 +175,13 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
         if (__ballot(stream && r <= last_round) == 0) break;
         // rounds <= r landed once at most the newest two rounds' 8 DMAs are in flight
         PROF_MARK(0);
+#if QLZX_K1_ROUND == 64
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+#elif QLZX_K1_ROUND == 32
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#else
+#error "QLZX_K1_ROUND: 32 or 64"
+#endif
         PROF_MARK(1);  // 1: waiting for the round's DMA
         const bool act = stream && r <= last_round;
         if (CRC && act) {  // CRC of this round's bytes, in stream order
@@ -196,34 +206,47 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
             _pacc[5] += 1;
             if (go) _pacc[6] += 1;
 #endif
-            // one step = a control word (k == 31) or one item: a match token or a
-            // literal run.  Straight-line selects; only the record store branches.
+            // one step = a control word (k == 31), or a literal run (possibly empty)
+            // followed by the match that ends it.  Straight-line selects; only the
+            // record store branches.
             const bool gb = k == 31;
             const uint32_t kk = k & 31;
             const uint32_t cwk = cw >> kk;
-            const uint32_t bit = gb ? 0u : (cwk & 1u);
-            const bool end = ip + (gb ? 4u : 1u) > csize;                   // stream exhausted
-            const bool stepping = go & !end & (ip + (gb ? 4u : bit) <= lim);  // bytes read have landed
-            const uint32_t w = ring_rd32(ring, ip + shift, lane);  // cword or token (unused for literals)
+            uint32_t run = __builtin_ctz(cwk | (1u << (31 - kk)));             // literals before the next match
+            run = gb ? 0u : (run < csize - ip ? run : csize - ip);
+            const uint32_t ipm = ip + run, km = kk + run;                       // the match after the run
+            const bool hasm = !gb & (km < 31) & (ipm < csize);
+            const bool end = ip + (gb ? 4u : 1u) > csize;                       // stream exhausted
+            const bool landed = ipm + (gb ? 4u : 1u) <= lim;                    // bytes this step reads
+            const bool mat = hasm & landed;
+            const bool stepping = go & !end & (gb ? landed : (run > 0) | mat);
+            const uint32_t w = ring_rd32(ring, ipm + shift, lane);  // cword, or the match token
             const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
             const uint32_t code = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);  // token bytes - 1
-            uint32_t run = __builtin_ctz(cwk | (1u << (31 - kk)));             // literal run to next match
-            run = run < csize - ip ? run : csize - ip;
+            // a second match right after it when its first byte is already in w
+            const uint32_t ip2 = ipm + code + 1, k2 = km + 1;
+            const uint32_t w2 = w >> (8 * ((code + 1) & 3));
+            const bool mat2 = mat & (code < 3) & (k2 < 31) & (((cw >> (k2 & 31)) & 1u) != 0) & (ip2 < csize) &
+                              (ip2 + 1 <= lim);
+            const uint32_t ty2 = (w2 & 3u) + ((w2 & 127u) == 3u ? 1u : 0u);
+            const uint32_t code2 = __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4);
             const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) |  // C1, group bound
-                                         ((bit != 0) & (ip + code + 1 > csize)));  // C2
+                                         (mat & (ipm + code + 1 > csize)) |        // C2
+                                         (mat2 & (ip2 + code2 + 1 > csize)));
             if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
             st = bad ? QLZX_E_CORRUPT : st;
             const bool adv = stepping & !bad;
             const bool ag = adv & gb;
-            const uint32_t bm = bit << kk;
+            const uint32_t bm = mat ? (1u << (km & 31)) : 0u;
+            const uint32_t bm2 = mat2 ? (1u << (k2 & 31)) : 0u;
             rec_ip = ag ? ip : rec_ip;
             cw = ag ? w : cw;
             g += ag ? 1u : 0u;
-            ip += adv ? (gb ? 4u : (bit ? code + 1 : run)) : 0u;
-            k = adv ? (gb ? 0u : k + (bit ? 1u : run)) : k;
-            m = adv ? (gb ? 0u : m | bm) : m;
-            ra = adv ? (gb ? 0u : ra | ((code & 1u) ? bm : 0u)) : ra;
-            rb = adv ? (gb ? 0u : rb | ((code & 2u) ? bm : 0u)) : rb;
+            ip += adv ? (gb ? 4u : run + (mat ? code + 1 : 0u) + (mat2 ? code2 + 1 : 0u)) : 0u;
+            k = adv ? (gb ? 0u : km + (mat ? 1u : 0u) + (mat2 ? 1u : 0u)) : k;
+            m = adv ? (gb ? 0u : m | bm | bm2) : m;
+            ra = adv ? (gb ? 0u : ra | ((code & 1u) ? bm : 0u) | ((code2 & 1u) ? bm2 : 0u)) : ra;
+            rb = adv ? (gb ? 0u : rb | ((code & 2u) ? bm : 0u) | ((code2 & 2u) ? bm2 : 0u)) : rb;
             done_parse = done_parse | (go & (end | bad));
             go = adv;
         }
