@@ -1,6 +1,9 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests -x -q -m gpu 2>&1 | tail -3 || exit 1
-QLZX_LIB=gobeansdb_amd/libqlzx_prof.so timeout -k 10 200 python tools/phase_prof.py 2>&1 | grep K1
-bash tools/prof.sh k1m --blocks 262144 --unique 16384 --steps 3 --warmup 1 --no-cpu | grep "k_dec" | cut -c1-40,150-260 || exit 1
+mkdir -p gpurun_out/r01b
+PMC_BENCH_ARGS="--blocks 131072 --steps 1 --warmup 0 --no-cpu" bash tools/pmc.sh r01b/pmc "FETCH_SIZE" "WRITE_SIZE" > gpurun_out/r01b/pmc.txt 2>&1 || { tail gpurun_out/r01b/pmc.txt; exit 1; }
+python tools/traffic.py gpurun_out/r01b/pmc 131072 gpurun_out/r01b/traffic.json > /dev/null
+timeout -k 10 600 python bench.py --traffic-json gpurun_out/r01b/traffic.json > gpurun_out/r01b/bench.json 2> gpurun_out/r01b/bench.err || { tail gpurun_out/r01b/bench.err; exit 1; }
+cat gpurun_out/r01b/bench.json
+bash tools/prof.sh r01b/prof --no-cpu --traffic-json gpurun_out/r01b/traffic.json | grep "k_dec" | cut -c1-50,140-260
