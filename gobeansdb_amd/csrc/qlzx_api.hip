@@ -11,11 +11,11 @@
 #include <string>
 
 #include "qlzx_tables.hip"
+#include "qlzx_crc.hip"
 #include "qlzx_decode_lane.hip"
 #include "qlzx_decode_wave.hip"
 #include "qlzx_encode_lane.hip"
 #include "qlzx_encode_wg.hip"
-#include "qlzx_crc.hip"
 #include "qlzx_replay.hip"
 #include "qlzx_record.hip"
 
@@ -127,7 +127,8 @@ int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_
 }
 
 size_t qlzx_compress_workspace_size(uint32_t n, uint32_t max_len) {
-    size_t ws = 0;
+    // at least one lane slab: QLZX_F_GO_COMPAT batches (flags are not known here) take the lane path
+    size_t ws = qlzx::kLaneSlab;
     if (max_len > QLZX_WG_MAX_LEN || !qlzx::encode_wg_enabled())
         ws = (size_t)std::min<uint32_t>(std::max<uint32_t>(n, 1), kMaxLaneSlabs) * qlzx::kLaneSlab;
     return std::max(ws, qlzx::encode_wg_ws_bytes(n, max_len));

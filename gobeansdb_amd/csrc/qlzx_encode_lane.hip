@@ -147,7 +147,7 @@ __global__ void __launch_bounds__(64) k_encode_lane(qlzx_blocks b, uint32_t *csi
     uint8_t *count = slab + (size_t)QLZX_BUCKETS * QLZX_SLOTS * 4;
     for (uint32_t i = t; i < b.n; i += nlanes) {
         const uint32_t n = b.src_len[i];
-        if (min_len && n < min_len && n > 0) continue;
+        if (min_len && n < min_len) continue;  // the workgroup kernel owns it (including n == 0)
         int st = QLZX_OK;
         uint8_t *dst = b.dst + b.dst_off[i];
         const uint32_t r = compress_block_lane(b.src + b.src_off[i], n, dst, slots, count, flags, st);

@@ -1,0 +1,129 @@
+"""GPU parity of the position-parallel workgroup encoder (k_encode_wg, csrc/qlzx_encode_wg.hip).
+
+Every output is compared byte for byte with the oracle (oracle/qlz_oracle.c, itself pinned to
+the reference quicklz.c by tests/golden) and the fused CRC with zlib.crc32 of the output.  The
+cases aim at the places where a position-parallel restatement of quicklz.c:197-494 could drift
+from the serial loop:
+  * hash-counter wrap at 256 insertions and the 16-slot ring (zero runs: one bucket for all)
+  * ties between equal-length candidates (small alphabets; quicklz.c:344 prefers the larger o)
+  * same-bucket positions inside one 64-position batch (periodic data)
+  * matches that jump over whole 64-position walker segments (long runs)
+  * the bail-out test at control-word boundaries (noisy text, quicklz.c:218)
+  * the stored-block proof on incompressible input (random bytes) and its near misses
+  * the 9-byte core minimum, the 3/9-byte header switch at 216 B and all three size classes
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 2, 3, 4, 5, 8, 9, 10, 11, 12, 13, 20, 31, 32, 33, 63, 64, 65, 100, 215, 216, 217, 255, 256,
+         257, 300, 1000, 4095, 4096, 4097, 10000, 16383, 16384, 16385, 30000, 65535, 65536]
+
+
+def _noisy(rng, base: bytes, frac: float) -> bytes:
+    a = np.frombuffer(base, np.uint8).copy()
+    hit = rng.random(len(a)) < frac
+    a[hit] = rng.integers(0, 256, int(hit.sum()), dtype=np.uint8)
+    return a.tobytes()
+
+
+def _patterns(rng, n):
+    out = [O.gen_text(5, n, n), O.gen_image(9, n, n), rng.integers(0, 256, n, dtype=np.uint8).tobytes(),
+           bytes(n)]
+    for per in (1, 2, 3, 4, 5, 7, 64, 300):
+        unit = rng.integers(0, 256, per, dtype=np.uint8).tobytes()
+        out.append((unit * (n // per + 1))[:n])
+    out.append(_noisy(rng, O.gen_text(6, n, n), 0.42))
+    out.append(_noisy(rng, O.gen_text(7, n, n), 0.15))
+    out.append(rng.integers(0, 3, n, dtype=np.uint8).tobytes())           # many equal-length ties
+    out.append(rng.choice(np.frombuffer(b"ab", np.uint8), n).tobytes())
+    # random with a repeated stretch: the stored proof must not fire on a compressible tail
+    r = bytearray(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    if n >= 64:
+        k = n // 3
+        r[n - k:] = r[:k]
+    out.append(bytes(r))
+    return out
+
+
+def _gpu_compress(blocks, crc_state=None, **kw):
+    import torch
+    from gobeansdb_amd import batch
+    src = batch.BlockBatch.from_bytes(blocks)
+    cs_t = None if crc_state is None else torch.tensor(np.asarray(crc_state, np.uint32).view(np.int32),
+                                                       device="cuda")
+    dst, csize, status, crc = batch.compress(src, crc_state=cs_t, want_crc=True, **kw)
+    torch.cuda.synchronize()
+    cs = csize.cpu().numpy().view(np.uint32)
+    return dst.to_bytes(cs), status.cpu().numpy(), crc.cpu().numpy().view(np.uint32)
+
+
+def _check(blocks, crc_state=None, **kw):
+    outs, st, crc = _gpu_compress(blocks, crc_state=crc_state, **kw)
+    for i, (b, o) in enumerate(zip(blocks, outs)):
+        assert st[i] == 0, (i, len(b), st[i])
+        exp = O.compress(b)
+        assert o == exp, (i, len(b), len(o), len(exp), o[:16].hex(), exp[:16].hex())
+        s = 0xFFFFFFFF if crc_state is None else crc_state[i]
+        assert int(crc[i]) == O.crc32_write(s, o) ^ 0xFFFFFFFF, i
+    return outs
+
+
+@pytest.mark.parametrize("cls", [4096, 16384, 65536])
+def test_wg_encoder_matches_oracle(cuda, cls):
+    rng = np.random.default_rng(cls)
+    blocks = []
+    for n in SIZES:
+        if n <= cls:
+            blocks += _patterns(rng, n)
+    _check(blocks, max_len=max(len(b) for b in blocks))
+
+
+def test_wg_encoder_mixed_batch_and_reuse(cuda):
+    """More 64 KiB blocks than persistent workgroups (each one encodes several), mixed sizes,
+    empty values and a custom CRC state."""
+    rng = np.random.default_rng(11)
+    blocks = []
+    for k in range(300):
+        n = [65536, 65536, 40000, 777, 16384][k % 5]
+        kind = k % 4
+        if kind == 0:
+            blocks.append(O.gen_text(21, k, n))
+        elif kind == 1:
+            blocks.append(O.gen_image(21, k, n))
+        elif kind == 2:
+            blocks.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        else:
+            blocks.append(_noisy(rng, O.gen_text(22, k, n), 0.3))
+    states = [int(x) for x in rng.integers(0, 2**32, len(blocks), dtype=np.uint64)]
+    _check(blocks, crc_state=states)
+    outs, st, crc = _gpu_compress([b"", b"x" * 300, b""])
+    assert list(st) == [7, 0, 7]   # QLZX_E_EMPTY (cquicklz.go:36 panics on an empty value)
+    assert outs[1] == O.compress(b"x" * 300)
+
+
+def test_wg_encoder_round_trip_on_device(cuda):
+    """compress -> decompress on the GPU at a larger count (size-independent property)."""
+    import torch
+    from gobeansdb_amd import batch
+    n, bs = 2048, 65536
+    plain = batch.synth("image", 77, [bs] * n)
+    comp, cs, st, _ = batch.compress(plain, max_len=bs)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    src = batch.BlockBatch(comp.data, comp.off, cs)
+    out = batch.BlockBatch.empty_for([bs] * n)
+    dsz, st2, _ = batch.decompress(src, out, max_dsize=bs)
+    torch.cuda.synchronize()
+    assert int((st2 != 0).sum()) == 0
+    assert torch.equal(out.data, plain.data)
+    # spot-check bytes against the oracle
+    h = comp.to_bytes(cs)
+    for i in (0, 1, 2, 3, 1000, 2047):
+        assert h[i] == O.compress(O.gen_image(77, i, bs))
+
