@@ -66,6 +66,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
     kind = args.kind or ("text" if args.mode == "decompress" else "image")
+    if args.mode == "compress":
+        return bench_compress(args, rank, world, dev, kind)
     n = args.blocks
     bs = args.block_size
     uniq = args.unique or n
@@ -192,12 +194,138 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def cpu_baseline(kind: str, bs: int, seconds: float):
+SEED = 0x5EED2026
+
+
+def bench_compress(args, rank, world, dev, kind):
+    """Config c3: compress every block of the rank's shard (1 M x 64 KiB image-like by default) with
+    the fused record CRC, inputs resident in HBM.  Verified before timing by a device round trip
+    (compress -> decompress == input) and a CRC recomputation over the outputs."""
+    from gobeansdb_amd import batch, shard
+    n, bs = args.blocks, args.block_size
+    first, _ = shard.weak_shard(rank, n)
+    t0 = time.time()
+    plain = batch.BlockBatch.empty_for([bs] * n, device=dev)
+    poff = plain.off.cpu().numpy().view(np.uint64)
+    for c0 in range(0, n, args.gen_chunk):
+        m = min(args.gen_chunk, n - c0)
+        part = batch.synth(kind, SEED, [bs] * m, first_id=first + c0, device=dev)
+        if bs % 256 == 0:   # contiguous packing: one copy per chunk
+            o = int(poff[c0])
+            plain.data[o:o + m * bs].copy_(part.data[:m * bs])
+        else:
+            for j in range(m):
+                o, q = int(poff[c0 + j]), int(part.off[j])
+                plain.data[o:o + bs].copy_(part.data[q:q + bs])
+        del part
+    dst = batch.BlockBatch.empty_for([bs] * n, device=dev, pad=400)   # CCompress allocates len+400
+    ws = batch.Workspace(dev)
+    crc_state = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    log(f"rank {rank}: generated {n} x {bs} B {kind} in {time.time() - t0:.1f}s")
+
+    # ---- correctness gate: round trip on the device, fused CRC == recomputed CRC ----
+    _, cs, st, crc = batch.compress(plain, dst, crc_state=crc_state, max_len=bs, workspace=ws)
+    torch.cuda.synchronize()
+    if int((st != 0).sum().item()):
+        raise SystemExit("compress status")
+    comp = batch.BlockBatch(dst.data, dst.off, cs)
+    if not torch.equal(batch.crc32(comp), crc):
+        raise SystemExit("fused CRC != recomputed CRC")
+    chk = 1 << 14
+    tmp = batch.BlockBatch.empty_for([bs] * chk, device=dev)
+    for c0 in range(0, n, chk):
+        m = min(chk, n - c0)
+        sub = batch.BlockBatch(dst.data, dst.off[c0:c0 + m], cs[c0:c0 + m])
+        out = batch.BlockBatch(tmp.data, tmp.off[:m], tmp.length[:m])
+        _, st2, _ = batch.decompress(sub, out, max_dsize=bs, workspace=ws)
+        o0 = int(poff[c0])
+        if int((st2 != 0).sum().item()) or not torch.equal(tmp.data[:m * bs], plain.data[o0:o0 + m * bs]):
+            raise SystemExit(f"round trip mismatch in blocks {c0}..{c0 + m}")
+    csum = int(cs.to(torch.int64).sum().item())
+    stored = int((dst.data[dst.off] & 1 == 0).sum().item())
+    log(f"device round trip verified; {stored}/{n} blocks stored, out/in {csum / (n * bs):.4f}")
+
+    stream = torch.cuda.current_stream()
+
+    def step():
+        batch.compress(plain, dst, crc_state=crc_state, max_len=bs, workspace=ws, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t_start = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        step()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t_start
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    wall, kern_ms = shard.max_over_ranks([wall, kern_ms], device=dev)
+    tot = shard.sum_over_ranks({"in_bytes": n * bs, "out_bytes": csum}, device=dev)
+    value = tot["in_bytes"] * args.steps / wall / 2**30
+    achieved = (n * bs + csum) / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    tj = args.traffic_json or os.path.join(ROOT, "profiles", "r01_c3_traffic.json")
+    if os.path.exists(tj) and kind == "image" and bs == 65536:
+        traffic = round(json.load(open(tj))["hbm_bytes_per_block"] * n)
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(kind, bs, args.cpu_seconds, mode="compress")
+    if rank == 0:
+        rec = {
+            "metric": "GiB/s device-resident QuickLZ decompress (+compress), batched 4-64 KiB values",
+            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(wall * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": f"c3: compress + fused CRC32 of {n} x {bs} B {kind}-like values per GPU "
+                                   f"({stored} stored), device-resident; value = input GiB/s",
+                       "blocks_per_gpu": n, "block_size": bs, "fused_crc": True,
+                       "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": n * bs + csum},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def cpu_baseline(kind: str, bs: int, seconds: float, mode: str = "decompress"):
     """Oracle decoder on the host cores over a bounded sample of the same workload."""
     from oracle import oracle as O
     threads = min(os.cpu_count() or 1, 16)
     L = O.lib()
-    nblk = 2048
+    nblk = 2048 if mode == "decompress" else 256
+    if mode == "compress":
+        plain = [O.gen_text(SEED, i, bs) if kind == "text" else O.gen_image(SEED, i, bs) for i in range(nblk)]
+        off_s, tot_s = _pack(plain)
+        off_d, tot_d = _pack([b"\0" * (bs + 400)] * nblk)
+        srcb = np.zeros(tot_s, np.uint8)
+        for o, p_ in zip(off_s, plain):
+            srcb[int(o): int(o) + len(p_)] = np.frombuffer(p_, np.uint8)
+        lens = np.asarray([len(p_) for p_ in plain], np.uint32)
+        dst = np.zeros(tot_d, np.uint8)
+        reps, ns = 0, 0.0
+        t_end = time.time() + seconds
+        while time.time() < t_end or reps == 0:
+            ns += L.orc_bench_compress(srcb.ctypes.data, off_s.ctypes.data, lens.ctypes.data, dst.ctypes.data,
+                                       off_d.ctypes.data, nblk, threads, 0)
+            reps += 1
+        gibs = reps * nblk * bs / (ns * 1e-9) / 2**30
+        return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+                "sample": f"{reps} passes over {nblk} x {bs} B {kind} blocks, oracle/qlz_oracle.c "
+                          f"orc_compress (no CRC), {threads} threads, -O2"}
     plain = [O.gen_text(0x5EED2026, i, bs) if kind == "text" else O.gen_image(0x5EED2026, i, bs)
              for i in range(nblk)]
     comp = [O.compress(p) for p in plain]
