@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -14,6 +15,7 @@
 #include "qlzx_crc.hip"
 #include "qlzx_decode_lane.hip"
 #include "qlzx_decode_wave.hip"
+#include "qlzx_decode_lane8.hip"
 #include "qlzx_encode_lane.hip"
 #include "qlzx_encode_wg.hip"
 #include "qlzx_replay.hip"
@@ -110,6 +112,16 @@ int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_
     if (!b->src || !b->src_off || !b->src_len || !b->dst || !b->dst_off)
         return fail(QLZX_R_BAD_ARG, "qlzx_decompress_batch: null block array");
     hipStream_t s = (hipStream_t)stream;
+    static const bool lane8 = [] {
+        const char *e = getenv("QLZX_DECODE");
+        return e && !strcmp(e, "lane8");
+    }();
+    if (lane8 && !crc_state && !crc_expect && !crc_out) {
+        hipLaunchKernelGGL(qlzx::k_dec_lane8, dim3((b->n + 255) / 256), dim3(256), 0, s, *b, dst_cap, dsize,
+                           status, 0u);
+        HIP_OK(hipGetLastError());
+        return QLZX_R_OK;
+    }
     const bool fast = qlzx::decode_wave_enabled() && workspace &&
                       workspace_bytes >= qlzx::decode_wave_ws_bytes(b->n, max_dsize);
     if (fast) {

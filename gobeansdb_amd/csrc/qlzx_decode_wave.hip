@@ -554,7 +554,11 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             const bool far = s < base;
             const bool spec = off < len || len > 16 || (far && s + len > base);  // byte / chunked path
             uint32_t fy[5] = {0, 0, 0, 0, 0};
+#ifdef QLZX_EXP_NOFAR  // experiment: far sources read garbage from LDS (timing only)
+            const bool fload = false;
+#else
             const bool fload = in && valid && ism && far && !spec;
+#endif
             if (__ballot(fload)) {
                 if (fload) far_load20(dst, s, d & 3u, dsize, fy);
             }

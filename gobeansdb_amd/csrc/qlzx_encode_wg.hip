@@ -13,17 +13,20 @@
 // greedy parse that picks which positions emit items is sequential, and it is
 // resolved by segment walkers with a fix-up pass.
 //
-// Per block (one workgroup, block + working set in LDS, input read once):
+// Per block (one workgroup, block + working set in LDS, input read once;
+// blocks are handed to persistent workgroups by a global ticket counter):
 //   S. stored-block proof (incompressible input): a bound on the
-//      bytes any parse could save, from a count of repeated 3-grams, shows the
-//      bail-out test of quicklz.c:218 must fire -> emit the stored block.
+//      bytes any parse could save, from a count of repeated 3-gram hashes
+//      (bitmap of no-return LDS ORs, then a popcount), shows the bail-out test
+//      of quicklz.c:218 must fire -> emit the stored block.
 //   0. input -> LDS.
-//   1. stable partition of positions by bucket group (hash >> 4, 256 groups)
-//      into a per-workgroup global scratch list (wave-ballot ranks).
-//   2. each wave takes groups dynamically and walks the group's positions in
-//      64-position batches with a 16-bucket x 16-slot ring (packed position +
-//      upper 12 fetch bits, so the 3-byte compare needs no input read);
-//      candidates from the same batch come from peer lanes (ballot match).
+//   1. the searched positions sorted by 12-bit bucket, stable in position
+//      (two LSD radix passes: low 4 hash bits, then the bucket group), into a
+//      per-workgroup global scratch list, plus each bucket's start in it.
+//   2. every position in parallel: its candidates are the preceding <= 16
+//      entries of its bucket in the sorted list; longest match wins, ties to
+//      the larger position.  No per-bucket serial walk, so a block whose
+//      positions all share one bucket (zeros, runs) spreads like any other.
 //      Result: best length per position in LDS, offset in global scratch.
 //   3. greedy parse: one walker per 64-position segment, converged by
 //      re-walking segments whose entry point changed (usually 1-2 rounds).
@@ -110,6 +113,101 @@ __host__ __device__ inline bool stored_proof(uint32_t n, uint32_t D) {
 }
 
 constexpr uint32_t kEncGroups = 256;  // bucket groups (hash >> 4), 16 buckets each
+constexpr uint32_t kParseRounds = 4;  // segment-walker rounds before the serial item walk
+
+// One pass of a stable LSD radix partition of the searched positions by
+// NB_LOG2 bits of their hash (starting at bit `shift`): out[] lists the
+// positions of in[] (or 0..P-1) grouped by key, each group in input order.
+// Each wave owns a contiguous input range; counters are [key][wave] so the
+// exclusive scan over them is stable.  cnt holds (1 << NB_LOG2) * W words.
+template <uint32_t W, uint32_t NB_LOG2, typename OUT>
+__device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t *in, OUT *out, uint32_t shift,
+                                 uint32_t *cnt, uint64_t *wsum, unsigned long long *sub = nullptr) {
+#ifdef QLZX_PROFILE
+#define SUB_MARK(k)                                                         \
+    do {                                                                    \
+        if (sub) {                                                          \
+            const unsigned long long _n = __builtin_amdgcn_s_memtime();     \
+            sub[k] += _n - sub[7];                                          \
+            sub[7] = _n;                                                    \
+        }                                                                   \
+    } while (0)
+#else
+#define SUB_MARK(k) do { } while (0)
+#endif
+    constexpr uint32_t T = 64 * W, NB = 1u << NB_LOG2, NC = NB * W;
+    constexpr uint32_t CPT = NC >= T ? NC / T : 1;  // counters per scanning thread
+    static_assert(NC % CPT == 0 && NC / CPT <= T, "counter layout");
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t ltm = (1ull << lane) - 1ull;
+    for (uint32_t k = tid; k < NC; k += T) cnt[k] = 0;
+    const uint32_t per = (P + 64 * W - 1) / (64 * W) * 64;
+    const uint32_t r0 = min(P, wave * per), r1 = min(P, r0 + per);
+    __syncthreads();
+    SUB_MARK(0);
+    constexpr uint32_t U = 4;  // 64-element batches per iteration: their list loads are in flight together
+    for (uint32_t base = r0; base < r1; base += 64 * U) {
+        uint32_t pv[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t j = base + 64 * u + lane;
+            pv[u] = j < r1 ? (in ? (uint32_t)in[j] : j) : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            if (base + 64 * u + lane < r1)
+                atomicAdd(&cnt[((hash12(fetch24(s_in, pv[u])) >> shift) & (NB - 1)) * W + wave], 1u);
+        }
+    }
+    __syncthreads();
+    SUB_MARK(1);  // count
+    {
+        const bool own = tid * CPT < NC;
+        uint32_t v[CPT];
+        uint32_t sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < CPT; j++) {
+            v[j] = own ? cnt[CPT * tid + j] : 0u;
+            sum += v[j];
+        }
+        uint64_t tot;
+        uint32_t ex = (uint32_t)block_scan_excl<W>(sum, wsum, tot);
+        if (own) {
+#pragma unroll
+            for (uint32_t j = 0; j < CPT; j++) {
+                cnt[CPT * tid + j] = ex;
+                ex += v[j];
+            }
+        }
+    }
+    __syncthreads();
+    SUB_MARK(2);  // scan
+    for (uint32_t base0 = r0; base0 < r1; base0 += 64 * U) {  // wave-uniform
+      uint32_t pv[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) {
+          const uint32_t j = base0 + 64 * u + lane;
+          pv[u] = j < r1 ? (in ? (uint32_t)in[j] : j) : 0u;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) {
+        const uint32_t j = base0 + 64 * u + lane;
+        const bool valid = j < r1;
+        const uint32_t p = pv[u];
+        const uint32_t f = fetch24(s_in, p);
+        const uint32_t key = valid ? (hash12(f) >> shift) & (NB - 1) : 0u;
+        const uint64_t peers = match_peers<NB_LOG2>(key, __ballot(valid));
+        const uint32_t intra = __popcll(peers & ltm);
+        uint32_t cur = 0;
+        if (valid) cur = cnt[key * W + wave];
+        // every lane's read is issued before the leader's write (in-order LDS per wave)
+        if (valid && intra == 0) cnt[key * W + wave] = cur + (uint32_t)__popcll(peers);
+        if (valid) out[cur + intra] = (OUT)(sizeof(OUT) == 2 ? p : p | ((f >> 12) << 16));
+      }
+    }
+    __syncthreads();
+    SUB_MARK(3);  // scatter
+}
 
 template <uint32_t CAP>
 struct WgCfg {
@@ -121,36 +219,48 @@ struct WgCfg {
     static constexpr uint32_t BM_LOG2 = CAP >= 65536 ? 20 : (CAP >= 16384 ? 18 : 16);  // proof bitmap bits
     static constexpr uint32_t NCW = (CAP + 30) / 31;
     static constexpr uint32_t SC1 = kEncGroups * W;  // phase 1 counters
-    static constexpr uint32_t SC2 = W * (256 + 16);  // phase 2 rings + counters
     static constexpr uint32_t SC4 = 2 * NCW;         // phase 4 control words + positions
-    static constexpr uint32_t SC12 = SC1 > SC2 ? SC1 : SC2;
-    static constexpr uint32_t SCR = SC12 > SC4 ? SC12 : SC4;
-    static constexpr size_t SLOT_BYTES = (size_t)CAP * 4;  // gpos u16[CAP] + goff u16[CAP]
+    static constexpr uint32_t SC3 = (T + 2) + 2 * T;  // phase 3 exits + serial-walk segment bits
+    static constexpr uint32_t SCR = SC1 > SC4 ? (SC1 > SC3 ? SC1 : SC3) : (SC4 > SC3 ? SC4 : SC3);
+    // gl u32[CAP] (sorted positions | fetch[23:12] << 16) | goff u16[CAP] | bst u16[4096]
+    static constexpr size_t SLOT_BYTES = (size_t)CAP * 6 + QLZX_BUCKETS * 2;
     static_assert((1u << BM_LOG2) / 8 <= U_B, "proof bitmap overlays s_in|s_l8");
 };
+
+// Next block for a persistent workgroup: one ticket per block from a global
+// counter (blocks differ in cost by 100x: stored-proof vs full parse), so the
+// expensive ones spread over the workgroups instead of a static stride.
+__device__ __forceinline__ uint32_t next_block(uint32_t *ticket, uint32_t *s_slot) {
+    __syncthreads();  // every thread has read the previous ticket
+    if (threadIdx.x == 0) *s_slot = atomicAdd(ticket, 1u);
+    __syncthreads();
+    return *s_slot;
+}
 
 template <uint32_t CAP>
 __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t *csize_out, int32_t *status,
                                                          const uint32_t *crc_state, uint32_t *crc_out,
-                                                         uint8_t *ws) {
+                                                         uint8_t *ws, uint32_t *ticket) {
     using C = WgCfg<CAP>;
     constexpr uint32_t T = C::T, W = C::W;
     __shared__ __attribute__((aligned(16))) uint8_t s_u[C::U_B];
     __shared__ __attribute__((aligned(16))) uint32_t s_scr[C::SCR];
-    __shared__ uint32_t s_gstart[kEncGroups + 1];
     __shared__ uint64_t s_wsum[W];
     __shared__ uint32_t s_misc[24];  // [0] next group, [1] proof count, [4..] CRC stripes
     uint8_t *const s_in = s_u, *const s_l8 = s_u + C::IN_B;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t ltm = (1ull << lane) - 1ull;
-    uint16_t *gpos = (uint16_t *)(ws + (size_t)blockIdx.x * C::SLOT_BYTES);
-    uint16_t *goff = gpos + CAP;
+    uint32_t *gl = (uint32_t *)(ws + (size_t)blockIdx.x * C::SLOT_BYTES);
+    uint16_t *goff = (uint16_t *)(gl + CAP);
+    uint16_t *bst = goff + CAP;  // sorted-list start of each bucket
 
-    for (uint32_t i = blockIdx.x; i < b.n; i += gridDim.x) {
-        const uint32_t n = b.src_len[i];
-        __syncthreads();        // LDS of the previous block is free
-        if (n > CAP) continue;  // general (lane) path
+    PROF_DECL
+#ifdef QLZX_PROFILE
+    unsigned long long _pacc_sub[16] = {};
+#endif
+    for (uint32_t i = next_block(ticket, &s_misc[22]); i < b.n; i = next_block(ticket, &s_misc[22])) {
+        const uint32_t n = b.src_len[i];  // LDS of the previous block is free (next_block synced)
+        if (n > CAP) continue;            // general (lane) path
         if (n == 0) {           // cquicklz.go:36 panics on &src[0]
             if (tid == 0) {
                 csize_out[i] = 0;
@@ -168,13 +278,13 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
         }
         bool stored = false;
 
+        PROF_MARK(0);  // 0: ticket + setup
         // ---- S. stored-block proof on incompressible input ----
         if (n >= 256 && (((uintptr_t)src) & 15u) == 0) {
             uint32_t *bm = (uint32_t *)s_u;
             constexpr uint32_t BMW = (1u << C::BM_LOG2) / 32;
             for (uint32_t k = tid * 4; k < BMW; k += T * 4) *(uint4 *)(bm + k) = make_uint4(0, 0, 0, 0);
             __syncthreads();
-            uint32_t dup = 0;
             const uint32_t ny = n - 2;  // positions holding a whole 3-gram
             for (uint32_t y0 = tid * 16; y0 < ny; y0 += T * 16) {
                 uint32_t w[5];
@@ -199,14 +309,20 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                         const uint32_t f = __builtin_amdgcn_alignbyte(w[j / 4 + 1], w[j / 4], j & 3) & 0xFFFFFFu;
                         const uint32_t h = (f * 0x9E3779B1u) >> (32 - C::BM_LOG2);
                         const uint32_t bit = 1u << (h & 31u);
-                        dup += (atomicOr(&bm[h >> 5], bit) & bit) ? 1u : 0u;
+                        atomicOr(&bm[h >> 5], bit);  // no return: D = ny - distinct hashes
                     }
                 }
             }
-            for (int m = 32; m >= 1; m >>= 1) dup += __shfl_xor(dup, m, 64);
-            if (lane == 0) atomicAdd(&s_misc[1], dup);
             __syncthreads();
-            stored = stored_proof(n, s_misc[1]);
+            uint32_t ones = 0;
+            for (uint32_t k = tid * 4; k < BMW; k += T * 4) {
+                const uint4 v = *(const uint4 *)(bm + k);
+                ones += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+            }
+            for (int m = 32; m >= 1; m >>= 1) ones += __shfl_xor(ones, m, 64);
+            if (lane == 0) atomicAdd(&s_misc[1], ones);
+            __syncthreads();
+            stored = stored_proof(n, ny - s_misc[1]);
             if (stored) {  // quicklz.c:722-727 from the global copy of the input
                 if ((((uintptr_t)dst) & 3u) == 0) {
                     const uint32_t tot = n + hdr, a0 = (hdr + 3u) & ~3u;
@@ -238,150 +354,73 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             __syncthreads();
 
             if (P) {
-                // ---- 1. stable partition of positions by bucket group ----
-                uint32_t *cnt1 = s_scr;  // [group * W + wave]
-                for (uint32_t k = tid; k < kEncGroups * W; k += T) cnt1[k] = 0;
-                const uint32_t per = (P + 64 * W - 1) / (64 * W) * 64;
-                const uint32_t r0 = min(P, wave * per), r1 = min(P, r0 + per);
-                __syncthreads();
-                for (uint32_t base = r0; base < r1; base += 64) {
-                    const uint32_t p = base + lane;
-                    if (p < r1) atomicAdd(&cnt1[(hash12(fetch24(s_in, p)) >> 4) * W + wave], 1u);
-                }
-                __syncthreads();
-                {
-                    uint32_t v[4];
-                    uint32_t sum = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        v[j] = cnt1[4 * tid + j];
-                        sum += v[j];
-                    }
-                    uint64_t tot;
-                    uint32_t ex = (uint32_t)block_scan_excl<W>(sum, s_wsum, tot);
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        cnt1[4 * tid + j] = ex;
-                        ex += v[j];
-                    }
-                }
-                __syncthreads();
-                for (uint32_t g = tid; g < kEncGroups; g += T) s_gstart[g] = cnt1[g * W];
-                if (tid == 0) s_gstart[kEncGroups] = P;
-                __syncthreads();
-                for (uint32_t base = r0; base < r1; base += 64) {  // wave-uniform
-                    const uint32_t p = base + lane;
-                    const bool valid = p < r1;
-                    const uint32_t g = valid ? hash12(fetch24(s_in, p)) >> 4 : 0u;
-                    const uint64_t peers = match_peers<8>(g, __ballot(valid));
-                    const uint32_t intra = __popcll(peers & ltm);
-                    uint32_t cur = 0;
-                    if (valid) cur = cnt1[g * W + wave];
-                    // every lane's read is issued before the leader's write (in-order LDS per wave)
-                    if (valid && intra == 0) cnt1[g * W + wave] = cur + (uint32_t)__popcll(peers);
-                    if (valid) gpos[cur + intra] = (uint16_t)p;
+                PROF_MARK(1);  // 1: proof + input load
+                // ---- 1. positions sorted by bucket, stable: LSD radix on the low 4 hash
+                //         bits, then on the bucket group (hash >> 4) ----
+#ifdef QLZX_PROFILE
+                unsigned long long *subA = _pacc_sub, *subB = _pacc_sub + 8;
+                subA[7] = subB[7] = __builtin_amdgcn_s_memtime();
+#else
+                unsigned long long *subA = nullptr, *subB = nullptr;
+#endif
+                stable_partition<W, 4>(s_in, P, nullptr, goff, 0, s_scr, s_wsum, subA);  // goff: scratch until phase 2
+#ifdef QLZX_PROFILE
+                subB[7] = __builtin_amdgcn_s_memtime();
+#endif
+                stable_partition<W, 8>(s_in, P, goff, gl, 4, s_scr, s_wsum, subB);
+                // bucket starts in the sorted list (only buckets that occur are read back)
+                for (uint32_t t = tid; t < P; t += T) {
+                    const uint32_t h = hash12(fetch24(s_in, gl[t] & 0xFFFFu));
+                    if (t == 0 || hash12(fetch24(s_in, gl[t - 1] & 0xFFFFu)) != h) bst[h] = (uint16_t)t;
                 }
                 __syncthreads();
 
-                // ---- 2. best match per position, group by group ----
-                uint32_t *ring = s_scr + wave * (256 + 16);  // [bucket(16)][slot(16)] = pos | fetch[23:12] << 16
-                uint32_t *cntb = ring + 256;                  // hash_counter (mod 256) per bucket
-                for (;;) {
-                    uint32_t g = 0;
-                    if (lane == 0) g = atomicAdd(&s_misc[0], 1u);
-                    g = __shfl(g, 0, 64);
-                    if (g >= kEncGroups) break;
-                    const uint32_t gs = s_gstart[g], ge = s_gstart[g + 1];
-                    if (gs == ge) continue;
-                    if (lane < 16) cntb[lane] = 0;
-                    for (uint32_t base = gs; base < ge; base += 64) {  // wave-uniform
-                        const uint32_t j = base + lane;
-                        const bool valid = j < ge;
-                        const uint32_t p = valid ? (uint32_t)gpos[j] : 0u;
-                        const uint32_t f = valid ? fetch24(s_in, p) : 0u;
-                        const uint32_t bk = hash12(f) & 15u, fh = f >> 12;
-                        const uint64_t peers = match_peers<4>(bk, __ballot(valid));
-                        const uint64_t below = peers & ltm;
-                        const uint32_t intra = __popcll(below);
-                        const uint32_t above = (uint32_t)__popcll(peers & ~ltm) - (valid ? 1u : 0u);
-                        const uint32_t c0 = valid ? cntb[bk] : 0u;
-                        const uint32_t r = c0 + intra;  // this position's insertion index (mod 256)
-                        const uint32_t rm = r & 255u;
-                        const uint32_t d = valid ? (rm < 16u ? rm : 16u) : 0u;  // candidates (c > k bound)
-                        const uint32_t dr = d > intra ? d - intra : 0u;        // of them in the ring
-                        const uint32_t limit = valid ? min(255u, n - 4u - p) : 0u;  // quicklz.c:310
-                        const uint32_t packed = p | (fh << 16);
-                        uint32_t best = 0, bpos = 0;
-                        // ring candidates: insertion ranks c0-dr .. c0-1 live in slots rank & 15
-                        uint32_t fm = 0;
-                        if (__ballot(dr != 0)) {
-                            const uint4 *row = (const uint4 *)(ring + bk * 16);
-#pragma unroll 1
-                            for (uint32_t q4 = 0; q4 < 4; q4++) {
-                                const uint4 v = row[q4];
-                                const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+                PROF_MARK(2);  // 2: sort by bucket
+                // ---- 2. best match per position, all positions in parallel ----
+                // The candidates of the position at sorted index t are the d most recent
+                // earlier positions of its bucket -- sorted indices t-1 .. t-d -- with
+                // d = min(rank mod 256, 16) (u8 hash_counter, c > k bound, quicklz.c:316-331).
+                // Longest wins, ties to the larger position (quicklz.c:344): scanning from
+                // the most recent, a candidate must be strictly longer, and a match of the
+                // full extension limit ends the scan.
+                for (uint32_t t = tid; t < P; t += T) {
+                    const uint32_t self = gl[t], p = self & 0xFFFFu, fh = self >> 16;
+                    const uint32_t rm = (t - (uint32_t)bst[hash12(fetch24(s_in, p))]) & 255u;
+                    const uint32_t d = rm < 16u ? rm : 16u;
+                    uint32_t cand[16];  // most recent first; all 16 loads in flight at once
 #pragma unroll
-                                for (uint32_t t = 0; t < 4; t++) {
-                                    const uint32_t s = 4 * q4 + t;
-                                    const bool ok = ((e[t] ^ (fh << 16)) < 0x10000u) && (((c0 - 1u - s) & 15u) < dr);
-                                    fm |= ok ? (1u << s) : 0u;
-                                }
-                            }
-                        }
-                        // same-batch candidates (peer lanes, most recent first), then the ring
-                        uint64_t tmp = below;
-                        uint32_t kk = 0;
+                    for (uint32_t k = 0; k < 16; k++) cand[k] = gl[k < d ? t - 1 - k : t];
+                    const uint32_t limit = min(255u, n - 4u - p);  // quicklz.c:310
+                    uint32_t best = 0, bpos = 0;
+#pragma unroll
+                    for (uint32_t k = 0; k < 16; k++) {
+                        const uint32_t q = cand[k] & 0xFFFFu;
+                        // same bucket + same fetch[23:12] = same 3 bytes; o < src - MINOFFSET
+                        if (k >= d || (cand[k] >> 16) != fh || q + 3u > p || best >= limit) continue;
+                        if (best && s_in[q + best] != s_in[p + best]) continue;
+                        uint32_t m = 3;
                         for (;;) {
-                            const bool use_intra = tmp != 0 && kk < d;
-                            if (__ballot(use_intra || fm != 0) == 0) break;
-                            uint32_t ei = 0;
-                            if (__ballot(use_intra)) {
-                                const int sl = use_intra ? 63 - __builtin_clzll(tmp) : (int)lane;
-                                ei = __shfl(packed, sl, 64);
-                                if (use_intra) tmp &= ~(1ull << sl);
+                            const uint32_t x = ld32u(s_in, q + m) ^ ld32u(s_in, p + m);
+                            if (x) {
+                                m += (uint32_t)__builtin_ctz(x) >> 3;
+                                break;
                             }
-                            uint32_t q = 0xFFFFFFFFu;
-                            if (use_intra) {
-                                kk++;
-                                if ((ei >> 16) == fh) q = ei & 0xFFFFu;
-                            } else if (fm) {
-                                const uint32_t s = __builtin_ctz(fm);
-                                fm &= fm - 1;
-                                q = ring[bk * 16 + s] & 0xFFFFu;
-                            }
-                            // quicklz.c:318-354: longest match, ties to the larger position
-                            // (candidates arrive in no particular order); o < src - MINOFFSET.
-                            // A lower position than the best so far must be strictly longer.
-                            if (q != 0xFFFFFFFFu && q + 3u <= p &&
-                                (best == 0 || q > bpos || (best < limit && s_in[q + best] == s_in[p + best]))) {
-                                uint32_t m = 3;
-                                for (;;) {
-                                    const uint32_t x = ld32u(s_in, q + m) ^ ld32u(s_in, p + m);
-                                    if (x) {
-                                        m += (uint32_t)__builtin_ctz(x) >> 3;
-                                        break;
-                                    }
-                                    m += 4;
-                                    if (m >= limit) break;
-                                }
-                                if (m > limit) m = limit;
-                                if (m > best || (m == best && q > bpos)) {
-                                    best = m;
-                                    bpos = q;
-                                }
-                            }
+                            m += 4;
+                            if (m >= limit) break;
                         }
-                        if (valid) {
-                            s_l8[p] = (uint8_t)best;  // 0 = literal, else 3..255
-                            if (best) goff[p] = (uint16_t)(p - bpos);
-                            if (above < 16u) ring[bk * 16 + (r & 15u)] = packed;  // quicklz.c:356-358
-                            if (above == 0u) cntb[bk] = (r + 1u) & 255u;
+                        if (m > limit) m = limit;
+                        if (m > best) {
+                            best = m;
+                            bpos = q;
                         }
                     }
+                    s_l8[p] = (uint8_t)best;  // 0 = literal, else 3..255
+                    if (best) goff[p] = (uint16_t)(p - bpos);
                 }
             }
             __syncthreads();
 
+            PROF_MARK(3);  // 3: best match per position
             // ---- 3. greedy parse (quicklz.c:361-372,449-485): segment walkers + fix-up ----
             const uint32_t nseg = (n + 63) / 64;
             const uint32_t s0 = tid * 64, e0 = min(n, s0 + 64);
@@ -441,8 +480,27 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     }
                 }
                 if (!__syncthreads_or(changed)) break;
+                if (round + 1 == kParseRounds) {
+                    // Not converged: long matches carry the parse across many segments
+                    // (runs, repeated stretches), one segment per round.  Such a parse has
+                    // few items, so one lane walks it from the start in item steps.
+                    uint64_t *sb = (uint64_t *)(s_scr + ((nseg + 1) & ~1u));
+                    for (uint32_t k = tid; k < nseg; k += T) sb[k] = 0;
+                    __syncthreads();
+                    if (tid == 0) {
+                        for (uint32_t p = 0; p < n;) {
+                            sb[p >> 6] |= 1ull << (p & 63u);
+                            const uint32_t L = p < P ? (uint32_t)s_l8[p] : 0u;
+                            p += L ? L : 1u;
+                        }
+                    }
+                    __syncthreads();
+                    if (tid < nseg) bits = sb[tid];
+                    break;
+                }
             }
 
+            PROF_MARK(4);  // 4: greedy parse
             // ---- 4. sizes, bail-out test, emission ----
             uint32_t items = 0, bytes = 0;
             if (tid < nseg) {
@@ -517,6 +575,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             }
         }
 
+        PROF_MARK(5);  // 5: sizes/bail/emission (or stored copy)
         // ---- 5. fused CRC of the emitted value (store/crc32.go:61-68) ----
         if (crc_state && crc_out) {
             __syncthreads();  // emitted bytes visible to the whole workgroup
@@ -539,11 +598,17 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 crc_out[i] = ~run;
             }
         }
+        PROF_MARK(6);  // 6: CRC
         if (tid == 0) {
             csize_out[i] = csz;
             if (status) status[i] = QLZX_OK;
         }
     }
+    PROF_FLUSH(2);
+#ifdef QLZX_PROFILE
+    if (g_prof && (threadIdx.x & 63) == 0)
+        for (int _j = 0; _j < 16; _j++) atomicAdd(&g_prof[24 + _j], _pacc_sub[_j]);
+#endif
 }
 
 inline bool encode_wg_enabled() { return true; }
@@ -555,10 +620,15 @@ inline uint32_t encode_wg_cap(uint32_t max_len) {
 // Persistent workgroups per class: LDS-bound residency x 256 CUs.
 inline uint32_t encode_wg_slots(uint32_t cap) { return cap == 65536 ? 256u : (cap == 16384 ? 1024u : 2560u); }
 
+inline size_t encode_wg_slot_bytes(uint32_t cap) {
+    return cap == 4096 ? WgCfg<4096>::SLOT_BYTES : (cap == 16384 ? WgCfg<16384>::SLOT_BYTES : WgCfg<65536>::SLOT_BYTES);
+}
+
+// [ticket counter, 256 B][slot 0][slot 1]...
 inline size_t encode_wg_ws_bytes(uint32_t n, uint32_t max_len) {
     const uint32_t cap = encode_wg_cap(max_len);
     const uint32_t slots = std::min<uint32_t>(std::max<uint32_t>(n, 1), encode_wg_slots(cap));
-    return (size_t)slots * cap * 4;
+    return 256 + (size_t)slots * encode_wg_slot_bytes(cap);
 }
 
 inline int launch_encode_wg(const qlzx_blocks &b, uint32_t *csize, int32_t *status, const uint32_t *crc_state,
@@ -567,13 +637,19 @@ inline int launch_encode_wg(const qlzx_blocks &b, uint32_t *csize, int32_t *stat
     const uint32_t cap = encode_wg_cap(max_len);
     const uint32_t grid = std::min<uint32_t>(b.n, encode_wg_slots(cap));
     if (grid == 0) return 0;
-    uint8_t *w = (uint8_t *)ws;
+    uint32_t *ticket = (uint32_t *)ws;
+    uint8_t *w = (uint8_t *)ws + 256;
+    hipError_t e = hipMemsetAsync(ticket, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return (int)e;
     if (cap == 4096)
-        hipLaunchKernelGGL(k_encode_wg<4096>, dim3(grid), dim3(64), 0, s, b, csize, status, crc_state, crc_out, w);
+        hipLaunchKernelGGL(k_encode_wg<4096>, dim3(grid), dim3(64), 0, s, b, csize, status, crc_state, crc_out, w,
+                           ticket);
     else if (cap == 16384)
-        hipLaunchKernelGGL(k_encode_wg<16384>, dim3(grid), dim3(256), 0, s, b, csize, status, crc_state, crc_out, w);
+        hipLaunchKernelGGL(k_encode_wg<16384>, dim3(grid), dim3(256), 0, s, b, csize, status, crc_state, crc_out, w,
+                           ticket);
     else
-        hipLaunchKernelGGL(k_encode_wg<65536>, dim3(grid), dim3(1024), 0, s, b, csize, status, crc_state, crc_out, w);
+        hipLaunchKernelGGL(k_encode_wg<65536>, dim3(grid), dim3(1024), 0, s, b, csize, status, crc_state, crc_out, w,
+                           ticket);
     return (int)hipGetLastError();
 }
 
