@@ -100,7 +100,9 @@ int qlz_get_setting(int setting) {  // quicklz.c:31-58 as built by quicklz.h:25-
 /* ---------------- batch device API ---------------- */
 
 size_t qlzx_decompress_workspace_size(uint32_t n, uint32_t max_dsize) {
-    return qlzx::decode_wave_ws_bytes(n, max_dsize);
+    // two halves for batches of more than one chunk: K1/K2 of consecutive chunks overlap
+    const size_t one = qlzx::decode_wave_ws_bytes(n, max_dsize);
+    return n > qlzx::kChunkBlocks ? 2 * one : one;
 }
 
 int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_t *dsize,

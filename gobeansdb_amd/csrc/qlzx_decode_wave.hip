@@ -655,28 +655,53 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
                               int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
                               uint32_t *crc_out, uint32_t max_dsize, void *ws, size_t ws_bytes,
                               hipStream_t s) {
-    (void)ws_bytes;
     const uint32_t md = max_dsize > QLZX_FAST_MAX_DSIZE ? QLZX_FAST_MAX_DSIZE : max_dsize;
     const uint32_t gmax = groups_max(md);
     const uint32_t chunk = b.n < kChunkBlocks ? b.n : kChunkBlocks;
-    BlkInfo *info = (BlkInfo *)ws;
     const size_t o_rec = ((size_t)chunk * sizeof(BlkInfo) + 255) & ~(size_t)255;
-    GroupRec *recs = (GroupRec *)((uint8_t *)ws + o_rec);
+    const size_t one = decode_wave_ws_bytes(b.n, max_dsize);
+    // two workspace halves when the caller gave room for them: K1 of chunk c+1 runs on a
+    // side stream while K2 of chunk c runs on `s` (K1 is latency-bound at low occupancy)
+    static const bool overlap_env = [] {  // QLZX_K1_OVERLAP=0: serial K1/K2 (experiments)
+        const char *e = getenv("QLZX_K1_OVERLAP");
+        return !(e && e[0] == '0');
+    }();
+    const bool overlap = overlap_env && ws_bytes >= 2 * one && b.n > chunk;
+    // per host thread (the batch API is re-entrant like the reference); the side stream
+    // belongs to the device that was current at the thread's first overlapped call
+    thread_local hipStream_t side = nullptr;
+    thread_local hipEvent_t ev_k1[2], ev_k2[2];
+    if (overlap && !side) {
+        if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) return (int)hipErrorUnknown;
+        for (int j = 0; j < 2; j++) {
+            (void)hipEventCreateWithFlags(&ev_k1[j], hipEventDisableTiming);
+            (void)hipEventCreateWithFlags(&ev_k2[j], hipEventDisableTiming);
+        }
+    }
     const bool crc = crc_state || crc_expect || crc_out;
-    for (uint32_t first = 0; first < b.n; first += chunk) {
+    if (overlap) (void)hipEventRecord(ev_k2[1], s), (void)hipStreamWaitEvent(side, ev_k2[1], 0);
+    uint32_t c = 0;
+    for (uint32_t first = 0; first < b.n; first += chunk, c++) {
         const uint32_t cnt = b.n - first < chunk ? b.n - first : chunk;
+        uint8_t *w = (uint8_t *)ws + (overlap ? (c & 1) * one : 0);
+        BlkInfo *info = (BlkInfo *)w;
+        GroupRec *recs = (GroupRec *)(w + o_rec);
+        hipStream_t s1 = overlap ? side : s;
+        if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
         if (crc)
-            hipLaunchKernelGGL(k_dec_parse<true>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s, b,
+            hipLaunchKernelGGL(k_dec_parse<true>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b,
                                dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax);
         else
-            hipLaunchKernelGGL(k_dec_parse<false>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s, b,
+            hipLaunchKernelGGL(k_dec_parse<false>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b,
                                dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax);
+        if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
 #ifndef QLZX_EXP_K2_EXTRA_LDS
 #define QLZX_EXP_K2_EXTRA_LDS 0  // experiments: extra dynamic LDS per WG to lower occupancy
 #endif
         // one kernel for every block size: the LDS window slides over longer blocks
         hipLaunchKernelGGL(k_dec_blocks<kWin>, dim3(cnt), dim3(64), QLZX_EXP_K2_EXTRA_LDS, s, b, dsize, status,
                            first, cnt, info, recs, gmax, (const uint32_t *)nullptr);
+        if (overlap) (void)hipEventRecord(ev_k2[c & 1], s);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }
