@@ -423,22 +423,20 @@ __device__ __forceinline__ uint32_t ff1_or(uint64_t m, uint32_t dflt) {
     return m ? (uint32_t)__builtin_ctzll(m) : dflt;
 }
 
-// Far source (below the window): 20 bytes from HBM starting at s - lo, as the five
-// destination-aligned dwords y[j] = bytes [s - lo + 4j, s - lo + 4j + 4) (the lo
-// leading bytes are masked off by the caller).  Loads are clamped inside [0, lim).
-__device__ __forceinline__ void far_load20(const uint8_t *dst, uint32_t s, uint32_t lo, uint32_t lim,
-                                           uint32_t y[5]) {
-    uint32_t x[5];
+// Far source (below the window): the five destination-aligned dwords
+// y[j] = bytes [a0 + 4j, a0 + 4j + 4) of the block's output in HBM, a0 = s - lo
+// (lo = the destination's byte offset in its dword, whose lo leading bytes the
+// caller masks off; callers guarantee s >= lo).  Unaligned dword loads straight
+// into y (no shuffle), so nothing waits on them until the first sub-round.
+// Dwords that hold needed bytes end <= d + 3 < dsize (check C3); later ones are
+// clamped inside [0, lim) and masked off.
+__device__ __forceinline__ void far_load20(const uint8_t *dst, uint32_t a0, uint32_t lim, uint32_t y[5]) {
 #pragma unroll
     for (int j = 0; j < 5; j++) {
-        uint32_t a = s + 4 * j;
+        uint32_t a = a0 + 4 * j;
         a = a + 4 <= lim ? a : lim - 4;
-        x[j] = *(const uint32_t *)(dst + a);  // unaligned dword load (unaligned access mode)
+        y[j] = *(const uint32_t *)(dst + a);  // unaligned dword load (unaligned access mode)
     }
-    const uint32_t sh = (4 - lo) & 3;
-    y[0] = lo ? __builtin_amdgcn_alignbyte(x[0], 0u, sh) : x[0];
-#pragma unroll
-    for (int j = 1; j < 5; j++) y[j] = lo ? __builtin_amdgcn_alignbyte(x[j], x[j - 1], sh) : x[j];
 }
 
 #ifndef QLZX_K2_WAVES_PER_EU
@@ -552,7 +550,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             // far sources (below the window, already in HBM): load them first, use them in the first sub-round
             const uint32_t s = d - off;
             const bool far = s < base;
-            const bool spec = off < len || len > 16 || (far && s + len > base);  // byte / chunked path
+            const bool spec = off < len || len > 16 || (far && (s + len > base || s < 3));  // byte / chunked path
             uint32_t fy[5] = {0, 0, 0, 0, 0};
 #ifdef QLZX_EXP_NOFAR  // experiment: far sources read garbage from LDS (timing only)
             const bool fload = false;
@@ -560,7 +558,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             const bool fload = in && valid && ism && far && !spec;
 #endif
             if (__ballot(fload)) {
-                if (fload) far_load20(dst, s, d & 3u, dsize, fy);
+                if (fload) far_load20(dst, s - (d & 3u), dsize, fy);
             }
             // ---- checks C2-C5 on the live items (those that start before dsize) ----
             const bool live = in && valid && d < dsize;
