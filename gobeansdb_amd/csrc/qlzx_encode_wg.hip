@@ -120,9 +120,16 @@ constexpr uint32_t kParseRounds = 4;  // segment-walker rounds before the serial
 // positions of in[] (or 0..P-1) grouped by key, each group in input order.
 // Each wave owns a contiguous input range; counters are [key][wave] so the
 // exclusive scan over them is stable.  cnt holds (1 << NB_LOG2) * W words.
+//   hist      (nullable) u16-pair histogram of the full 12-bit hash, counted
+//             in this pass's count loop (bucket starts, bucket_sort)
+//   next_cnt  (nullable) [key'][wave'] counts of the NEXT pass (key' = hash >> 4,
+//             wave' = the wave owning the output index), accumulated while
+//             scattering so the next pass needs no count loop
+//   counted   cnt already holds this pass's counts (from the previous scatter)
 template <uint32_t W, uint32_t NB_LOG2, typename OUT>
 __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t *in, OUT *out, uint32_t shift,
-                                 uint32_t *cnt, uint64_t *wsum, unsigned long long *sub = nullptr) {
+                                 uint32_t *cnt, uint64_t *wsum, unsigned long long *sub, uint32_t *hist,
+                                 uint32_t *next_cnt, bool counted) {
 #ifdef QLZX_PROFILE
 #define SUB_MARK(k)                                                         \
     do {                                                                    \
@@ -140,26 +147,32 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
     static_assert(NC % CPT == 0 && NC / CPT <= T, "counter layout");
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t ltm = (1ull << lane) - 1ull;
-    for (uint32_t k = tid; k < NC; k += T) cnt[k] = 0;
     const uint32_t per = (P + 64 * W - 1) / (64 * W) * 64;
     const uint32_t r0 = min(P, wave * per), r1 = min(P, r0 + per);
-    __syncthreads();
-    SUB_MARK(0);
+    const uint32_t per_magic = 0xFFFFFFFFu / per + 1u;  // umulhi(x, per_magic) = x / per for x < 2^16
     constexpr uint32_t U = 4;  // 64-element batches per iteration: their list loads are in flight together
-    for (uint32_t base = r0; base < r1; base += 64 * U) {
-        uint32_t pv[U];
+    SUB_MARK(0);
+    if (!counted) {
+        for (uint32_t k = tid; k < NC; k += T) cnt[k] = 0;
+        __syncthreads();
+        for (uint32_t base = r0; base < r1; base += 64 * U) {
+            uint32_t pv[U];
 #pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-            const uint32_t j = base + 64 * u + lane;
-            pv[u] = j < r1 ? (in ? (uint32_t)in[j] : j) : 0u;
-        }
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t j = base + 64 * u + lane;
+                pv[u] = j < r1 ? (in ? (uint32_t)in[j] : j) : 0u;
+            }
 #pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-            if (base + 64 * u + lane < r1)
-                atomicAdd(&cnt[((hash12(fetch24(s_in, pv[u])) >> shift) & (NB - 1)) * W + wave], 1u);
+            for (uint32_t u = 0; u < U; u++) {
+                if (base + 64 * u + lane < r1) {
+                    const uint32_t h = hash12(fetch24(s_in, pv[u]));
+                    atomicAdd(&cnt[((h >> shift) & (NB - 1)) * W + wave], 1u);
+                    if (hist) atomicAdd(&hist[h >> 1], 1u << (16 * (h & 1u)));
+                }
+            }
         }
+        __syncthreads();
     }
-    __syncthreads();
     SUB_MARK(1);  // count
     {
         const bool own = tid * CPT < NC;
@@ -195,18 +208,65 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
         const bool valid = j < r1;
         const uint32_t p = pv[u];
         const uint32_t f = fetch24(s_in, p);
-        const uint32_t key = valid ? (hash12(f) >> shift) & (NB - 1) : 0u;
+        const uint32_t h = hash12(f);
+        const uint32_t key = valid ? (h >> shift) & (NB - 1) : 0u;
         const uint64_t peers = match_peers<NB_LOG2>(key, __ballot(valid));
         const uint32_t intra = __popcll(peers & ltm);
         uint32_t cur = 0;
         if (valid) cur = cnt[key * W + wave];
         // every lane's read is issued before the leader's write (in-order LDS per wave)
         if (valid && intra == 0) cnt[key * W + wave] = cur + (uint32_t)__popcll(peers);
-        if (valid) out[cur + intra] = (OUT)(sizeof(OUT) == 2 ? p : p | ((f >> 12) << 16));
+        if (valid) {
+            out[cur + intra] = (OUT)(sizeof(OUT) == 2 ? p : p | ((f >> 12) << 16));
+            if (next_cnt) atomicAdd(&next_cnt[(h >> 4) * W + __umulhi(cur + intra, per_magic)], 1u);
+        }
       }
     }
     __syncthreads();
     SUB_MARK(3);  // scatter
+}
+
+// Searched positions sorted by 12-bit bucket, stable in position (two LSD radix
+// passes: low 4 hash bits, then the bucket group), as gl[t] = pos | fetch[23:12] << 16,
+// plus bst[h] = the sorted index where bucket h starts (exclusive scan of the
+// bucket histogram counted in the first pass).  tmp: u16[P] scratch; s_hist:
+// 2048 words of LDS free during the sort; s_cnt: 272 * W words.
+template <uint32_t W>
+__device__ void bucket_sort(const uint8_t *s_in, uint32_t P, uint16_t *tmp, uint32_t *gl, uint16_t *bst,
+                            uint32_t *s_cnt, uint32_t *s_hist, uint64_t *wsum, unsigned long long *subA,
+                            unsigned long long *subB) {
+    constexpr uint32_t T = 64 * W;
+    const uint32_t tid = threadIdx.x;
+    uint32_t *cntB = s_cnt, *cntA = s_cnt + kEncGroups * W;
+    for (uint32_t k = tid; k < QLZX_BUCKETS / 2; k += T) s_hist[k] = 0;
+    for (uint32_t k = tid; k < kEncGroups * W; k += T) cntB[k] = 0;
+    // (pass A zeroes its own counters and syncs before counting)
+    stable_partition<W, 4>(s_in, P, nullptr, tmp, 0, cntA, wsum, subA, s_hist, cntB, false);
+    // bucket starts: exclusive scan of the u16-pair histogram, bucket order = sorted order
+    {
+        constexpr uint32_t PT = QLZX_BUCKETS / 2 / T > 0 ? QLZX_BUCKETS / 2 / T : 1;  // words per thread
+        const bool own = tid * PT < QLZX_BUCKETS / 2;
+        uint32_t sum = 0;
+        if (own)
+            for (uint32_t j = 0; j < PT; j++) {
+                const uint32_t w = s_hist[tid * PT + j];
+                sum += (w & 0xFFFFu) + (w >> 16);
+            }
+        uint64_t tot;
+        uint32_t ex = (uint32_t)block_scan_excl<W>(sum, wsum, tot);
+        if (own)
+            for (uint32_t j = 0; j < PT; j++) {
+                const uint32_t w = s_hist[tid * PT + j], h0 = 2 * (tid * PT + j);
+                bst[h0] = (uint16_t)ex;
+                ex += w & 0xFFFFu;
+                bst[h0 + 1] = (uint16_t)ex;
+                ex += w >> 16;
+            }
+    }
+#ifdef QLZX_PROFILE
+    if (subB) subB[7] = __builtin_amdgcn_s_memtime();
+#endif
+    stable_partition<W, 8>(s_in, P, tmp, gl, 4, cntB, wsum, subB, nullptr, nullptr, true);
 }
 
 template <uint32_t CAP>
@@ -218,7 +278,7 @@ struct WgCfg {
     static constexpr uint32_t U_B = IN_B + L8_B;                          // s_in | s_l8
     static constexpr uint32_t BM_LOG2 = CAP >= 65536 ? 20 : (CAP >= 16384 ? 18 : 16);  // proof bitmap bits
     static constexpr uint32_t NCW = (CAP + 30) / 31;
-    static constexpr uint32_t SC1 = kEncGroups * W;  // phase 1 counters
+    static constexpr uint32_t SC1 = (kEncGroups + 16) * W;  // phase 1 counters (both radix passes)
     static constexpr uint32_t SC4 = 2 * NCW;         // phase 4 control words + positions
     static constexpr uint32_t SC3 = (T + 2) + 2 * T;  // phase 3 exits + serial-walk segment bits
     static constexpr uint32_t SCR = SC1 > SC4 ? (SC1 > SC3 ? SC1 : SC3) : (SC4 > SC3 ? SC4 : SC3);
@@ -363,17 +423,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
 #else
                 unsigned long long *subA = nullptr, *subB = nullptr;
 #endif
-                stable_partition<W, 4>(s_in, P, nullptr, goff, 0, s_scr, s_wsum, subA);  // goff: scratch until phase 2
-#ifdef QLZX_PROFILE
-                subB[7] = __builtin_amdgcn_s_memtime();
-#endif
-                stable_partition<W, 8>(s_in, P, goff, gl, 4, s_scr, s_wsum, subB);
-                // bucket starts in the sorted list (only buckets that occur are read back)
-                for (uint32_t t = tid; t < P; t += T) {
-                    const uint32_t h = hash12(fetch24(s_in, gl[t] & 0xFFFFu));
-                    if (t == 0 || hash12(fetch24(s_in, gl[t - 1] & 0xFFFFu)) != h) bst[h] = (uint16_t)t;
-                }
-                __syncthreads();
+                bucket_sort<W>(s_in, P, goff, gl, bst, s_scr, (uint32_t *)s_l8, s_wsum, subA, subB);
 
                 PROF_MARK(2);  // 2: sort by bucket
                 // ---- 2. best match per position, all positions in parallel ----
@@ -391,14 +441,32 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
 #pragma unroll
                     for (uint32_t k = 0; k < 16; k++) cand[k] = gl[k < d ? t - 1 - k : t];
                     const uint32_t limit = min(255u, n - 4u - p);  // quicklz.c:310
-                    uint32_t best = 0, bpos = 0;
+                    // First pass: bytes 3..6 of every candidate against this position's, all 16
+                    // LDS reads independent.  A mismatch there gives the exact length; the
+                    // candidates equal through byte 6 ("long") are extended afterwards, most
+                    // recent first -- they beat every short one, and ties stay with the more
+                    // recent (larger) position.
+                    const uint32_t P3 = ld32u(s_in, p + 3);
+                    uint32_t best = 0, bpos = 0, longm = 0;
 #pragma unroll
                     for (uint32_t k = 0; k < 16; k++) {
                         const uint32_t q = cand[k] & 0xFFFFu;
                         // same bucket + same fetch[23:12] = same 3 bytes; o < src - MINOFFSET
-                        if (k >= d || (cand[k] >> 16) != fh || q + 3u > p || best >= limit) continue;
-                        if (best && s_in[q + best] != s_in[p + best]) continue;
-                        uint32_t m = 3;
+                        const bool ok = k < d && (cand[k] >> 16) == fh && q + 3u <= p;
+                        const uint32_t x = ld32u(s_in, q + 3) ^ P3;
+                        const uint32_t m = min(x ? 3u + ((uint32_t)__builtin_ctz(x) >> 3) : 7u, limit);
+                        if (ok && !x && limit > 7u) longm |= 1u << k;
+                        else if (ok && m > best) {
+                            best = m;
+                            bpos = q;
+                        }
+                    }
+                    if (longm) best = 0;  // a long candidate always wins
+                    while (longm && best < limit) {
+                        const uint32_t k = (uint32_t)__builtin_ctz(longm);
+                        longm &= longm - 1u;
+                        const uint32_t q = gl[t - 1 - k] & 0xFFFFu;
+                        uint32_t m = 7;
                         for (;;) {
                             const uint32_t x = ld32u(s_in, q + m) ^ ld32u(s_in, p + m);
                             if (x) {
