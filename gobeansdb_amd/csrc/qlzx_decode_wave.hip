@@ -279,13 +279,15 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
 }
 
 // ------------------------------------------------------------------ K2 ----
-// mem = (mem & ~mask) | val in one LDS instruction (val pre-masked).
+// mem = (mem & ~mask) | val in one LDS instruction (val pre-masked); OFF = byte
+// offset folded into the instruction (one address register for a whole copy).
+template <uint32_t OFF = 0>
 __device__ __forceinline__ void lds_mskor(uint32_t *addr, uint32_t mask, uint32_t val) {
     const uint32_t a = (uint32_t)(uintptr_t)addr;
 #ifdef QLZX_EXP_PLAINWRITE  // experiment: plain dword stores (wrong bytes; timing only)
-    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(val | mask) : "memory");
+    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(a), "v"(val | mask), "i"(OFF) : "memory");
 #else
-    asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(a), "v"(mask), "v"(val) : "memory");
+    asm volatile("ds_mskor_b32 %0, %1, %2 offset:%3" ::"v"(a), "v"(mask), "v"(val), "i"(OFF) : "memory");
 #endif
 }
 
@@ -294,11 +296,11 @@ __device__ __forceinline__ void lds_mskor(uint32_t *addr, uint32_t mask, uint32_
 // flushed to the block's destination in HBM ("window").
 template <uint32_t W>
 struct K2Lds {
+    uint8_t pad[16];                 // a source dword may start 4 B before win[0]
+    uint8_t win[W + 32];             // reads run <= 24 B past a write; win[W + 24] = literal dummy
     GroupRec rec[kRecSlots][4];      // records of the <= 4 groups of batches bt+4..bt+8
     uint32_t tok[kTokSlots][64];     // per-lane token dword of batches bt..bt+3
-    uint8_t win[W + 32];             // a source dword may start 4 B before win[0] (reads tok);
-                                     // reads run <= 24 B past a write; win[W + 24] = literal dummy
-};
+};  // the window first: copy addresses fit the DS instructions' immediate offsets
 
 // Every K2 iteration issues exactly 2 DMA instructions (1 token dword + 1
 // record), with dummy addresses for lanes/batches past the end, so that
@@ -390,21 +392,21 @@ struct Copy16 {
         const uint32_t v3 = far ? y[3] : __builtin_amdgcn_alignbyte(x4, x3, sh);
         const uint32_t v4 = far ? y[4] : __builtin_amdgcn_alignbyte(x5, x4, sh);
         uint32_t *dw = (uint32_t *)(out + qa);
-        lds_mskor(dw + 0, mk[0], v0 & mk[0]);
-        lds_mskor(dw + 1, mk[1], v1 & mk[1]);
-        lds_mskor(dw + 2, mk[2], v2 & mk[2]);
-        lds_mskor(dw + 3, mk[3], v3 & mk[3]);
-        lds_mskor(dw + 4, mk[4], v4 & mk[4]);
+        lds_mskor<0>(dw, mk[0], v0 & mk[0]);
+        lds_mskor<4>(dw, mk[1], v1 & mk[1]);
+        lds_mskor<8>(dw, mk[2], v2 & mk[2]);
+        lds_mskor<12>(dw, mk[3], v3 & mk[3]);
+        lds_mskor<16>(dw, mk[4], v4 & mk[4]);
     }
     __device__ __forceinline__ void run(uint8_t *out) const {
         const uint32_t *x = (const uint32_t *)(out + xa);
         const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4], x5 = x[5];
         uint32_t *dw = (uint32_t *)(out + qa);
-        lds_mskor(dw + 0, mk[0], __builtin_amdgcn_alignbyte(x1, x0, sh) & mk[0]);
-        lds_mskor(dw + 1, mk[1], __builtin_amdgcn_alignbyte(x2, x1, sh) & mk[1]);
-        lds_mskor(dw + 2, mk[2], __builtin_amdgcn_alignbyte(x3, x2, sh) & mk[2]);
-        lds_mskor(dw + 3, mk[3], __builtin_amdgcn_alignbyte(x4, x3, sh) & mk[3]);
-        lds_mskor(dw + 4, mk[4], __builtin_amdgcn_alignbyte(x5, x4, sh) & mk[4]);
+        lds_mskor<0>(dw, mk[0], __builtin_amdgcn_alignbyte(x1, x0, sh) & mk[0]);
+        lds_mskor<4>(dw, mk[1], __builtin_amdgcn_alignbyte(x2, x1, sh) & mk[1]);
+        lds_mskor<8>(dw, mk[2], __builtin_amdgcn_alignbyte(x3, x2, sh) & mk[2]);
+        lds_mskor<12>(dw, mk[3], __builtin_amdgcn_alignbyte(x4, x3, sh) & mk[3]);
+        lds_mskor<16>(dw, mk[4], __builtin_amdgcn_alignbyte(x5, x4, sh) & mk[4]);
     }
 };
 

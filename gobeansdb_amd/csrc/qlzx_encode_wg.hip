@@ -602,7 +602,18 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             }
             bail = __syncthreads_or(bail);
             if (bail) {  // stored block (quicklz.c:722-727)
-                for (uint32_t o = tid; o < n; o += T) dst[hdr + o] = s_in[o];
+                if ((((uintptr_t)dst) & 15u) == 0) {  // 16-B stores from the LDS copy of the input
+                    const uint32_t tot = n + hdr, a0 = (hdr + 15u) & ~15u, a1 = tot & ~15u;
+                    for (uint32_t o = a0 + tid * 16; o < a1; o += T * 16) {
+                        const uint32_t q = o - hdr;
+                        *(uint4 *)(dst + o) = make_uint4(ld32u(s_in, q), ld32u(s_in, q + 4), ld32u(s_in, q + 8),
+                                                         ld32u(s_in, q + 12));
+                    }
+                    for (uint32_t o = hdr + tid; o < tot; o += T)
+                        if (o < a0 || o >= a1) dst[o] = s_in[o - hdr];
+                } else {
+                    for (uint32_t o = tid; o < n; o += T) dst[hdr + o] = s_in[o];
+                }
                 if (tid == 0) write_header(dst, hdr, false, n + hdr, n);
                 csz = n + hdr;
             } else {
