@@ -47,7 +47,10 @@ struct GroupRec {
 
 constexpr int32_t kPending = -1;  // status of blocks left to the general path
 constexpr uint32_t kBlkSkip = 0, kBlkStored = 1, kBlkCompressed = 2;
-constexpr uint32_t kParseWG = 64;          // K1 workgroup: one wave (LDS per wave bounds occupancy)
+// K1 workgroup: one wave (the 16 KiB LDS ring per wave bounds occupancy); with the CRC,
+// four waves share one 8 KiB slicing-by-8 table (8 waves/CU instead of 6)
+template <bool CRC>
+constexpr uint32_t kParseWG = CRC ? 256 : 64;
 constexpr uint32_t kChunkBlocks = 131072;  // >= 256 CUs x 8 waves x 64 lanes: K1 fills the chip
 #ifndef QLZX_K1_ROUND
 #define QLZX_K1_ROUND 64
@@ -109,20 +112,20 @@ __device__ __forceinline__ void ring_issue(uint8_t *ring_wave, const uint8_t *gb
 }
 
 template <bool CRC>
-__global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uint32_t *dst_cap,
+__global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, const uint32_t *dst_cap,
                                                          uint32_t *dsize_out, int32_t *status,
                                                          const uint32_t *crc_state, const uint32_t *crc_expect,
                                                          uint32_t *crc_out, uint32_t first, uint32_t count,
                                                          BlkInfo *info, GroupRec *recs, uint32_t gmax) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG / 64) * kRingWave];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG<CRC> / 64) * kRingWave];
     __shared__ uint32_t tab[CRC ? 8 * 256 : 1];
     if (CRC) {
-        for (uint32_t t = threadIdx.x; t < 8 * 256; t += kParseWG) tab[t] = g_crc_slice8[t];
+        for (uint32_t t = threadIdx.x; t < 8 * 256; t += kParseWG<CRC>) tab[t] = g_crc_slice8[t];
         __syncthreads();
     }
     const uint32_t lane = threadIdx.x & 63;
     uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWave;
-    const uint32_t li = blockIdx.x * kParseWG + threadIdx.x;
+    const uint32_t li = blockIdx.x * kParseWG<CRC> + threadIdx.x;
     const bool inrange = li < count;
     const uint32_t i = first + (inrange ? li : 0);
 
@@ -689,10 +692,12 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         hipStream_t s1 = overlap ? side : s;
         if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
         if (crc)
-            hipLaunchKernelGGL(k_dec_parse<true>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b,
+            hipLaunchKernelGGL(k_dec_parse<true>, dim3((cnt + kParseWG<true> - 1) / kParseWG<true>),
+                               dim3(kParseWG<true>), 0, s1, b,
                                dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax);
         else
-            hipLaunchKernelGGL(k_dec_parse<false>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b,
+            hipLaunchKernelGGL(k_dec_parse<false>, dim3((cnt + kParseWG<false> - 1) / kParseWG<false>),
+                               dim3(kParseWG<false>), 0, s1, b,
                                dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax);
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
 #ifndef QLZX_EXP_K2_EXTRA_LDS
