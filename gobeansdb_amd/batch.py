@@ -96,8 +96,10 @@ class Workspace:
 def decompress(src: BlockBatch, dst: BlockBatch, *, dst_cap: torch.Tensor | None = None,
                crc_state: torch.Tensor | None = None, crc_expect: torch.Tensor | None = None,
                want_crc: bool = False, max_dsize: int | None = None,
-               workspace: Workspace | None = None, stream=None):
-    """Batch CDecompressSafe.  Returns (dsize u32, status i32, crc_out u32|None) device tensors."""
+               workspace: Workspace | None = None, stream=None, general: bool = False):
+    """Batch CDecompressSafe.  Returns (dsize u32, status i32, crc_out u32|None) device tensors.
+    general=True passes no workspace, which routes every block to the general lane-per-block
+    kernel (the path of values over 64 KiB); used by the parity tests of that kernel."""
     L = _lib.lib()
     n = src.n
     dev = src.data.device
@@ -106,12 +108,12 @@ def decompress(src: BlockBatch, dst: BlockBatch, *, dst_cap: torch.Tensor | None
     crc_out = torch.zeros(n, dtype=torch.int32, device=dev) if (want_crc or crc_expect is not None) else None
     if max_dsize is None:
         max_dsize = 0xFFFFFFFF
-    ws_bytes = L.qlzx_decompress_workspace_size(n, max_dsize)
-    ws = (workspace or Workspace(dev)).get(ws_bytes)
+    ws_bytes = 0 if general else L.qlzx_decompress_workspace_size(n, max_dsize)
+    ws_ptr = None if general else (workspace or Workspace(dev)).get(ws_bytes).data_ptr()
     b = _blocks(src, dst.data, dst.off)
     rc = L.qlzx_decompress_batch(ctypes.byref(b), _ptr(dst_cap), dsize.data_ptr(), status.data_ptr(),
                                  _ptr(crc_state), _ptr(crc_expect), _ptr(crc_out), max_dsize,
-                                 ws.data_ptr(), ws_bytes, _stream(stream))
+                                 ws_ptr, ws_bytes, _stream(stream))
     _lib.check(rc, "qlzx_decompress_batch")
     return dsize, status, crc_out
 

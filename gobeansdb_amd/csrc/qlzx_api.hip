@@ -13,7 +13,6 @@
 
 #include "qlzx_tables.hip"
 #include "qlzx_crc.hip"
-#include "qlzx_decode_lane.hip"
 #include "qlzx_decode_wave.hip"
 #include "qlzx_decode_lane8.hip"
 #include "qlzx_encode_lane.hip"
@@ -118,13 +117,8 @@ int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_
         const char *e = getenv("QLZX_DECODE");
         return e && !strcmp(e, "lane8");
     }();
-    if (lane8 && !crc_state && !crc_expect && !crc_out) {
-        hipLaunchKernelGGL(qlzx::k_dec_lane8, dim3((b->n + 255) / 256), dim3(256), 0, s, *b, dst_cap, dsize,
-                           status, 0u);
-        HIP_OK(hipGetLastError());
-        return QLZX_R_OK;
-    }
-    const bool fast = qlzx::decode_wave_enabled() && workspace &&
+    // QLZX_DECODE=lane8 (experiments) or no workspace: the general lane-per-block kernel for every block
+    const bool fast = !lane8 && qlzx::decode_wave_enabled() && workspace &&
                       workspace_bytes >= qlzx::decode_wave_ws_bytes(b->n, max_dsize);
     if (fast) {
         int r = qlzx::launch_decode_wave(*b, dst_cap, dsize, status, crc_state, crc_expect, crc_out,
@@ -133,7 +127,7 @@ int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_
     }
     if (!fast || max_dsize > QLZX_FAST_MAX_DSIZE) {
         const uint32_t min_dsize = fast ? QLZX_FAST_MAX_DSIZE + 1 : 0;
-        hipLaunchKernelGGL(qlzx::k_decode_lane, dim3((b->n + 255) / 256), dim3(256), 0, s, *b, dst_cap,
+        hipLaunchKernelGGL(qlzx::k_dec_lane8, dim3((b->n + 255) / 256), dim3(256), 0, s, *b, dst_cap,
                            dsize, status, crc_state, crc_expect, crc_out, min_dsize);
         HIP_OK(hipGetLastError());
     }

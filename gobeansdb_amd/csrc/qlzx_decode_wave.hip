@@ -618,6 +618,10 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                         }
                     }
                 }
+#ifdef QLZX_EXP_ONESUB  // experiment: every pending match copies in the first sub-round (timing only)
+                if (!ready && !done && !spec) cp.run_sel(win, far, fy);
+                done = true;
+#endif
                 done = done || ready;
                 // no lgkmcnt wait: a wave's LDS operations execute in issue order, so the
                 // next sub-round's reads observe these writes

@@ -55,9 +55,11 @@ def test_compress_golden_bit_exact(cuda, golden):
         assert int(c) == v["crc_c_out"], v["name"]   # fused CRC over the compressed value
 
 
-def test_decompress_golden(cuda, golden):
+# general=True: every block through the general lane-per-block kernel (values over 64 KiB)
+@pytest.mark.parametrize("general", [False, True])
+def test_decompress_golden(cuda, golden, general):
     vs = golden.vectors
-    outs, st, crc = _gpu_decompress([golden.get(v["c_out"]) for v in vs], want_crc=True)
+    outs, st, crc = _gpu_decompress([golden.get(v["c_out"]) for v in vs], want_crc=True, general=general)
     assert (st == 0).all(), [(v["name"], s) for v, s in zip(vs, st) if s]
     for v, o, c in zip(vs, outs, crc):
         assert o == golden.get(v["input"]), v["name"]
@@ -105,7 +107,8 @@ def test_cdecompress_safe_errors(cuda, golden):
     assert err is None and len(arr.Body) == 4096
 
 
-def test_corrupt_status_matches_oracle(cuda, golden):
+@pytest.mark.parametrize("general", [False, True])
+def test_corrupt_status_matches_oracle(cuda, golden, general):
     rng = np.random.default_rng(5)
     base = [golden.get(v["c_out"]) for v in golden.vectors if v["cls"] in ("text", "runs", "kat") and v["n"] >= 100]
     cases = []
@@ -119,7 +122,7 @@ def test_corrupt_status_matches_oracle(cuda, golden):
         cases.append(c[:-1])
     caps = [_dsize(c) for c in cases]
     caps = [min(x, 1 << 20) for x in caps]
-    outs, st, _ = _gpu_decompress(cases, caps=caps)
+    outs, st, _ = _gpu_decompress(cases, caps=caps, general=general)
     for c, cap, o, s in zip(cases, caps, outs, st):
         ost, od = O.decompress(c, cap=cap)
         assert s == ost
@@ -162,7 +165,8 @@ def test_go_compat_compress(cuda):
         assert o == O.compress_go(b)
 
 
-def test_record_fused_crc_verify(cuda, golden):
+@pytest.mark.parametrize("general", [False, True])
+def test_record_fused_crc_verify(cuda, golden, general):
     """store/datafile.go:161-168: CRC over header[4:24] ‖ key ‖ value, fused with decompress."""
     import struct
     import torch
@@ -183,7 +187,7 @@ def test_record_fused_crc_verify(cuda, golden):
     comp[1] = bytes(bad)
     s_t = torch.tensor(np.asarray(states, np.uint32).view(np.int32), device="cuda")
     e_t = torch.tensor(np.asarray(expect, np.uint32).view(np.int32), device="cuda")
-    outs, st, crc = _gpu_decompress(comp, crc_state=s_t, crc_expect=e_t)
+    outs, st, crc = _gpu_decompress(comp, crc_state=s_t, crc_expect=e_t, general=general)
     for i, (o, s, v) in enumerate(zip(outs, st, values)):
         if i == 1:
             assert s == 5   # QLZX_E_CRC
