@@ -28,6 +28,9 @@ extern __device__ uint32_t g_crc_pow[64];
 extern __device__ uint32_t g_crc_slice8[8 * 256];
 // g_crc_piece[k] = x^(8 * 64 * k) mod P: shift of a 64-B piece's CRC over k later 64-B pieces.
 extern __device__ uint32_t g_crc_piece[64];
+// g_crc_byte[j] = x^(8 j); g_crc_stripe[k] = x^(8 * 4096 * k).
+extern __device__ uint32_t g_crc_byte[64];
+extern __device__ uint32_t g_crc_stripe[64];
 
 constexpr uint32_t CRC_POLY = 0xEDB88320u;
 
@@ -52,6 +55,11 @@ __device__ __forceinline__ uint32_t crc_shift(uint32_t s, uint64_t nbytes) {
         k++;
     }
     return s;
+}
+
+// x^(8 n) for n <= 4096 in at most one product (tables above).
+__device__ __forceinline__ uint32_t crc_xpow_bytes(uint32_t n) {
+    return n == 4096 ? g_crc_pow[12] : gf2_mulmod(g_crc_piece[n >> 6], g_crc_byte[n & 63]);
 }
 
 __device__ __forceinline__ uint32_t crc_byte(const uint32_t *tab, uint32_t c, uint32_t b) {

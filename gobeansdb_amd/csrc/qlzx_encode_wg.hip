@@ -668,13 +668,19 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 if (lane == 0) s_misc[4 + st] = raw;
             }
             __syncthreads();
-            if (tid == 0) {
-                uint32_t run = crc_state[i];
-                for (uint32_t st = 0; st < nst; st++) {
-                    const uint32_t len = min(4096u, csz - st * 4096);
-                    run = (len == 4096 ? gf2_mulmod(g_crc_pow[12], run) : crc_shift(run, len)) ^ s_misc[4 + st];
+            // Combine in one wave, every stripe at once: with L = the last stripe's length,
+            //   raw = (state * x^(8*4096*(nst-1)) ^ XOR_{s<nst-1} raw_s * x^(8*4096*(nst-2-s))) * x^(8L)
+            //         ^ raw_{nst-1}
+            // (a stripe's CRC shifted over the bytes after it; the state over all of them).
+            if (wave == 0) {
+                uint32_t v = 0;
+                if (lane + 1 < nst) v = gf2_mulmod(g_crc_stripe[nst - 2 - lane], s_misc[4 + lane]);
+                else if (lane == 63) v = gf2_mulmod(g_crc_stripe[nst - 1], crc_state[i]);
+                for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
+                if (lane == 0) {
+                    const uint32_t last = csz - (nst - 1) * 4096;  // 1..4096
+                    crc_out[i] = ~(gf2_mulmod(crc_xpow_bytes(last), v) ^ s_misc[4 + nst - 1]);
                 }
-                crc_out[i] = ~run;
             }
         }
         PROF_MARK(6);  // 6: CRC

@@ -7,6 +7,8 @@ struct CrcTables {
     uint32_t table[256];
     uint32_t pow8[64];
     uint32_t piece[64];  // piece[k] = x^(8 * 64 * k): shifts a 64-B piece's CRC over k later pieces
+    uint32_t byte[64];   // byte[j] = x^(8 * j): with piece[], x^(8 n) for n < 4096 in one product
+    uint32_t stripe[64]; // stripe[k] = x^(8 * 4096 * k): shifts a 4 KiB stripe's CRC over k stripes
     uint32_t slice[8][256];  // slice[k][b]: CRC of byte b followed by k zero bytes (slicing-by-8)
 };
 
@@ -42,6 +44,10 @@ __host__ __device__ constexpr CrcTables make_tables() {
     }
     t.piece[0] = 0x80000000u;  // x^0
     for (int k = 1; k < 64; k++) t.piece[k] = mulmod_c(t.piece[k - 1], t.pow8[6]);  // * x^(8*64)
+    t.byte[0] = 0x80000000u;
+    for (int k = 1; k < 64; k++) t.byte[k] = mulmod_c(t.byte[k - 1], t.pow8[0]);     // * x^8
+    t.stripe[0] = 0x80000000u;
+    for (int k = 1; k < 64; k++) t.stripe[k] = mulmod_c(t.stripe[k - 1], t.pow8[12]);  // * x^(8*4096)
     return t;
 }
 
@@ -86,6 +92,14 @@ __device__ uint32_t g_crc_piece[64] = {
 #undef Q8
 #undef Q
 };
+
+#define T8(a, i) kTables.a[i], kTables.a[i + 1], kTables.a[i + 2], kTables.a[i + 3], kTables.a[i + 4], \
+    kTables.a[i + 5], kTables.a[i + 6], kTables.a[i + 7]
+#define T64(a) T8(a, 0), T8(a, 8), T8(a, 16), T8(a, 24), T8(a, 32), T8(a, 40), T8(a, 48), T8(a, 56)
+__device__ uint32_t g_crc_byte[64] = {T64(byte)};
+__device__ uint32_t g_crc_stripe[64] = {T64(stripe)};
+#undef T64
+#undef T8
 
 }  // namespace qlzx
 
