@@ -571,13 +571,28 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             PROF_MARK(4);  // 4: greedy parse
             // ---- 4. sizes, bail-out test, emission ----
             uint32_t items = 0, bytes = 0;
+            uint32_t szc[4] = {0, 0, 0, 0};  // item sizes - 1, 2 bits per item of the segment (in order)
             if (tid < nseg) {
                 items = __popcll(bits);
-                for (uint64_t t = bits; t; t &= t - 1) {
-                    const uint32_t p = s0 + (uint32_t)__builtin_ctzll(t);
-                    const uint32_t L = p < P ? (uint32_t)s_l8[p] : 0u;
-                    uint32_t tk;
-                    bytes += L ? token_of(L, goff[p], tk) : 1u;
+                uint32_t j = 0;
+                for (uint64_t t = bits; t;) {  // four items per iteration: their offset loads overlap
+                    uint32_t p4[4], L4[4], o4[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        p4[u] = t ? s0 + (uint32_t)__builtin_ctzll(t) : 0xFFFFFFFFu;
+                        t &= t - 1;
+                        L4[u] = p4[u] < P ? (uint32_t)s_l8[p4[u]] : 0u;
+                        o4[u] = L4[u] ? (uint32_t)goff[p4[u]] : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (p4[u] == 0xFFFFFFFFu) break;
+                        uint32_t tk;
+                        const uint32_t sz = L4[u] ? token_of(L4[u], o4[u], tk) : 1u;
+                        bytes += sz;
+                        szc[j >> 4] |= (sz - 1u) << (2 * (j & 15));
+                        j++;
+                    }
                 }
             }
             uint64_t tot;
@@ -586,12 +601,11 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             const uint32_t Itot = (uint32_t)(tot >> 32), Btot = (uint32_t)tot;
             int bail = 0;
             if (tid < nseg) {  // quicklz.c:216-219: at each new control word inside the main loop
-                uint32_t idx = I0, bb = B0;
-                for (uint64_t t = bits; t; t &= t - 1) {
+                uint32_t idx = I0, bb = B0, j = 0;
+                for (uint64_t t = bits; t; t &= t - 1, j++) {
                     const uint32_t p = s0 + (uint32_t)__builtin_ctzll(t);
-                    const uint32_t L = p < P ? (uint32_t)s_l8[p] : 0u;
-                    uint32_t tk;
-                    const uint32_t sz = L ? token_of(L, goff[p], tk) : 1u;
+                    const uint32_t sw = (j >> 4) == 0 ? szc[0] : (j >> 4) == 1 ? szc[1] : (j >> 4) == 2 ? szc[2] : szc[3];
+                    const uint32_t sz = ((sw >> (2 * (j & 15))) & 3u) + 1u;
                     if (idx && idx % 31u == 0 && p < P) {
                         const uint32_t op = 4u * (idx / 31u) + bb;
                         if (p > 3u * (n >> 2) && op > p - (p >> 5)) bail = 1;
