@@ -193,3 +193,34 @@ def test_record_fused_crc_verify(cuda, golden, general):
             assert s == 5   # QLZX_E_CRC
         else:
             assert s == 0 and o == v
+
+
+@pytest.mark.parametrize("crc", [False, True])
+def test_multi_chunk_overlap_round_trip(cuda, crc):
+    """More blocks than one decode chunk (131072): K1 of chunk c+1 runs on the side stream while K2
+    of chunk c runs (two workspace halves).  Every block must round-trip, and with crc the fused
+    record CRC must equal a separate CRC pass over the compressed values."""
+    import torch
+    from gobeansdb_amd import batch
+    n = 131072 + 9000
+    lens = [256 + (i * 37) % 1800 for i in range(n)]
+    plain = batch.synth("text", 77, lens)
+    comp, cs, st, _ = batch.compress(plain, max_len=max(lens))
+    assert int((st != 0).sum()) == 0
+    src = batch.BlockBatch(comp.data, comp.off, cs)
+    out = batch.BlockBatch.empty_for(lens)
+    kw = {}
+    if crc:
+        kw = dict(crc_state=torch.full((n,), -1, dtype=torch.int32, device="cuda"), want_crc=True)
+    dsz, st2, crc_out = batch.decompress(src, out, max_dsize=max(lens), **kw)
+    torch.cuda.synchronize()
+    assert int((st2 != 0).sum()) == 0
+    assert torch.equal(dsz, plain.length)
+    # every valid byte (same lengths -> same packing; the padding between blocks is not compared)
+    ln = plain.length.to(torch.int64)
+    starts = torch.cumsum(ln, 0) - ln
+    rel = torch.arange(int(ln.sum()), device="cuda") - torch.repeat_interleave(starts, ln)
+    pos = torch.repeat_interleave(plain.off, ln) + rel
+    assert torch.equal(out.data[pos], plain.data[pos])
+    if crc:
+        assert torch.equal(crc_out, batch.crc32(src))
