@@ -15,6 +15,7 @@ Prints one JSON line (rank 0).  See DESIGN.md §6 for the roofline accounting.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -301,11 +302,17 @@ def bench_compress(args, rank, world, dev, kind):
         torch.distributed.destroy_process_group()
 
 
+REF_WHAT = ("reference quicklz/quicklz.c {fn} (oracle/_ref/libqlzref.so, gcc -O2 as cgo builds it), "
+            "per-thread scratch")
+
+
 def cpu_baseline(kind: str, bs: int, seconds: float, mode: str = "decompress"):
     """Oracle decoder on the host cores over a bounded sample of the same workload."""
     from oracle import oracle as O
     threads = min(os.cpu_count() or 1, 16)
     L = O.lib()
+    Q = O.ref_if_built()  # the reference quicklz.c (oracle/_ref) when built; else the C restatement
+    kind_ = "reference" if Q is not None else "port"
     nblk = 2048 if mode == "decompress" else 256
     if mode == "compress":
         plain = [O.gen_text(SEED, i, bs) if kind == "text" else O.gen_image(SEED, i, bs) for i in range(nblk)]
@@ -319,13 +326,19 @@ def cpu_baseline(kind: str, bs: int, seconds: float, mode: str = "decompress"):
         reps, ns = 0, 0.0
         t_end = time.time() + seconds
         while time.time() < t_end or reps == 0:
-            ns += L.orc_bench_compress(srcb.ctypes.data, off_s.ctypes.data, lens.ctypes.data, dst.ctypes.data,
-                                       off_d.ctypes.data, nblk, threads, 0)
+            if Q is not None:
+                ns += L.orc_bench_ref(ctypes.cast(Q.qlz_compress, ctypes.c_void_p).value, srcb.ctypes.data,
+                                      off_s.ctypes.data, lens.ctypes.data, dst.ctypes.data, off_d.ctypes.data,
+                                      nblk, threads, 1)
+            else:
+                ns += L.orc_bench_compress(srcb.ctypes.data, off_s.ctypes.data, lens.ctypes.data,
+                                           dst.ctypes.data, off_d.ctypes.data, nblk, threads, 0)
             reps += 1
         gibs = reps * nblk * bs / (ns * 1e-9) / 2**30
-        return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-                "sample": f"{reps} passes over {nblk} x {bs} B {kind} blocks, oracle/qlz_oracle.c "
-                          f"orc_compress (no CRC), {threads} threads, -O2"}
+        what = REF_WHAT.format(fn="qlz_compress") if Q is not None else "oracle/qlz_oracle.c orc_compress"
+        return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": kind_,
+                "sample": f"{reps} passes over {nblk} x {bs} B {kind} blocks, {what} (no CRC), "
+                          f"{threads} threads, -O2"}
     plain = [O.gen_text(0x5EED2026, i, bs) if kind == "text" else O.gen_image(0x5EED2026, i, bs)
              for i in range(nblk)]
     comp = [O.compress(p) for p in plain]
@@ -339,13 +352,20 @@ def cpu_baseline(kind: str, bs: int, seconds: float, mode: str = "decompress"):
     reps, ns = 0, 0.0
     t_end = time.time() + seconds
     while time.time() < t_end or reps == 0:
-        ns += L.orc_bench_decompress(srcb.ctypes.data, off_c.ctypes.data, lens.ctypes.data, dst.ctypes.data,
-                                     off_d.ctypes.data, nblk, threads, 0)
+        if Q is not None:
+            ns += L.orc_bench_ref(ctypes.cast(Q.qlz_decompress, ctypes.c_void_p).value, srcb.ctypes.data,
+                                  off_c.ctypes.data, lens.ctypes.data, dst.ctypes.data, off_d.ctypes.data,
+                                  nblk, threads, 0)
+        else:
+            ns += L.orc_bench_decompress(srcb.ctypes.data, off_c.ctypes.data, lens.ctypes.data,
+                                         dst.ctypes.data, off_d.ctypes.data, nblk, threads, 0)
         reps += 1
+    if Q is not None and not all(dst[int(o): int(o) + bs].tobytes() == p_ for o, p_ in zip(off_d[:8], plain[:8])):
+        raise RuntimeError("reference decompress baseline produced wrong bytes")
     gibs = reps * nblk * bs / (ns * 1e-9) / 2**30
-    return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} passes over {nblk} x {bs} B {kind} blocks, oracle/qlz_oracle.c "
-                      f"orc_decompress, {threads} threads, -O2"}
+    what = REF_WHAT.format(fn="qlz_decompress") if Q is not None else "oracle/qlz_oracle.c orc_decompress"
+    return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": kind_,
+            "sample": f"{reps} passes over {nblk} x {bs} B {kind} blocks, {what}, {threads} threads, -O2"}
 
 
 def _pack(blocks):

@@ -145,6 +145,19 @@ def ref():
     return _ref
 
 
+def ref_if_built():
+    """The compiled reference codec if oracle/_ref holds it (never builds: the GPU box
+    has no /root/reference, only the .so built here); None otherwise."""
+    q = os.path.join(HERE, "_ref", "libqlzref.so")
+    if not os.path.exists(q):
+        return None
+    Q = ctypes.CDLL(q)
+    L = lib()
+    L.orc_bench_ref.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
+    L.orc_bench_ref.restype = ctypes.c_double
+    return Q
+
+
 def ref_compress(data: bytes) -> bytes:
     Q, _ = ref()
     src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)

@@ -364,3 +364,52 @@ double orc_bench_compress(const uint8_t *src, const uint64_t *src_off, const uin
                           int cgo_faithful) {
     return run_threads(src, src_off, src_len, dst, dst_off, n, threads, cgo_faithful, 1);
 }
+
+/* ---------------- reference timing harness ----------------
+ * Times the REFERENCE codec (oracle/_ref/libqlzref.so, quicklz.c compiled from
+ * /root/reference by oracle/Makefile) through the function pointers bench.py
+ * passes in: qlz_decompress(src, dst, scratch) / qlz_compress(src, dst, size,
+ * scratch), the calls quicklz/cquicklz.go:23-101 make.  Each thread owns the
+ * reference's scratch (16 B decompress, 528,400 B compress: quicklz.h:
+ * QLZ_SCRATCH_*), allocated once, as a long-lived cgo caller would. */
+typedef size_t (*ref_dec_fn)(const char *, void *, char *);
+typedef size_t (*ref_comp_fn)(const void *, char *, size_t, char *);
+typedef struct {
+    const uint8_t *src; const uint64_t *src_off; const uint32_t *src_len;
+    uint8_t *dst; const uint64_t *dst_off;
+    uint32_t lo, hi; void *fn; int mode;
+} rjob_t;
+
+static void *run_rjob(void *arg) {
+    rjob_t *j = (rjob_t *)arg;
+    char *scratch = (char *)malloc(j->mode ? 528400 : 16);
+    if (j->mode) memset(scratch, 0, 528400);
+    for (uint32_t i = j->lo; i < j->hi; i++) {
+        const uint8_t *s = j->src + j->src_off[i];
+        uint8_t *d = j->dst + j->dst_off[i];
+        if (j->mode == 0) ((ref_dec_fn)j->fn)((const char *)s, d, scratch);
+        else ((ref_comp_fn)j->fn)(s, (char *)d, j->src_len[i], scratch);
+    }
+    free(scratch);
+    return NULL;
+}
+
+double orc_bench_ref(void *fn, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                     uint8_t *dst, const uint64_t *dst_off, uint32_t n, int threads, int mode) {
+    if (threads < 1) threads = 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+    rjob_t *jobs = (rjob_t *)malloc(sizeof(rjob_t) * threads);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (rjob_t){src, src_off, src_len, dst, dst_off,
+                           (uint32_t)((uint64_t)n * t / threads),
+                           (uint32_t)((uint64_t)n * (t + 1) / threads), fn, mode};
+        pthread_create(&th[t], NULL, run_rjob, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(th);
+    free(jobs);
+    return (t1.tv_sec - t0.tv_sec) * 1e9 + (t1.tv_nsec - t0.tv_nsec);
+}

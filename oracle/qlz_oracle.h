@@ -68,6 +68,9 @@ double orc_bench_compress(const uint8_t *src, const uint64_t *src_off,
                           const uint32_t *src_len, uint8_t *dst,
                           const uint64_t *dst_off, uint32_t n, int threads,
                           int cgo_faithful);
+/* times the reference codec through fn (qlz_decompress when mode 0, qlz_compress when 1) */
+double orc_bench_ref(void *fn, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                     uint8_t *dst, const uint64_t *dst_off, uint32_t n, int threads, int mode);
 
 #ifdef __cplusplus
 }
