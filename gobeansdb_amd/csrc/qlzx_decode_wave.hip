@@ -68,6 +68,7 @@ constexpr uint32_t kTokAhead = kK2Slack + 1;   // tokens of batch bt + 4 issued 
 constexpr uint32_t kRecAhead = 2 * kTokAhead;  // records of batch bt + 8 issued in iteration bt
 constexpr uint32_t kTokSlots = kTokAhead;      // batches bt .. bt+3 (bt+4 reuses bt's slot)
 constexpr uint32_t kRecSlots = kTokAhead + 1;  // batches bt+4 .. bt+8
+constexpr uint32_t kSubMax = 64 * 32;          // K2 sub-batch output bound: the 64-word item-start bitmap
 #ifndef QLZX_K2_VMWAIT
 #define QLZX_K2_VMWAIT 6  // = 2 * kK2Slack; experiments only: other values break the prefetch invariant
 #endif
@@ -424,6 +425,13 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+// Lane owning byte D + r of the sub-batch (r < kSubMax): starts at or before r, minus one.
+__device__ __forceinline__ uint32_t owner_of(const uint32_t *bm, uint32_t bex, uint32_t r) {
+    const uint32_t w = bm[r >> 5];
+    const uint32_t below = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((r >> 5) << 2), (int)bex);
+    return below + __builtin_popcount(w & ((2u << (r & 31)) - 1u)) - 1u;
+}
+
 __device__ __forceinline__ uint32_t ff1_or(uint64_t m, uint32_t dflt) {
     return m ? (uint32_t)__builtin_ctzll(m) : dflt;
 }
@@ -509,9 +517,13 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
         const uint32_t posm = pm[0];
 #pragma unroll
         for (uint32_t j = 0; j + 1 < kTokAhead; j++) pm[j] = pm[j + 1];
-        pm[kTokAhead - 1] = issue_tok(gr4, cur, v4, L.tok[ts], src, csize);
+        // the token DMA of batch bt+4 goes out at the end of the iteration: until then
+        // this batch's token slot holds the item-start bitmap of the sub-batches
+        uint32_t tokp;
+        pm[kTokAhead - 1] = issue_tok<false>(gr4, cur, v4, nullptr, src, csize, &tokp);
         cur.next();
         issue_rec(L.rec[rs8], rb, ((bt + kRecAhead) * 64) / 31, ngroups, lane);
+        uint32_t *const bm = L.tok[ts];
         ts = ts == kTokSlots - 1 ? 0 : ts + 1;
         rs4 = rs4 == kRecSlots - 1 ? 0 : rs4 + 1;
         rs8 = rs8 == kRecSlots - 1 ? 0 : rs8 + 1;
@@ -528,6 +540,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
         uint32_t lo_lane = 0;
         bool more = true;
         while (more) {
+            const uint32_t sub0 = lo_lane;  // first lane of this sub-batch
             const bool act = lane >= lo_lane;
             const uint32_t len = act ? len0 : 0u;
             uint32_t incl = wave_incl_scan(len);
@@ -545,7 +558,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             }
             const uint32_t d = D + incl - len;
             // this sub-batch: the active lanes whose output fits the window (a prefix)
-            const bool fits = d + len <= base + W;
+            const bool fits = d + len <= base + W && d + len <= D + kSubMax;
             const uint64_t outm = __ballot(act && len && !fits);
             const uint32_t cut = outm ? (uint32_t)__builtin_ctzll(outm) : 64u;
             const bool in = act && lane < cut;
@@ -581,24 +594,36 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             PROF_MARK(2);  // 2: decode + scan + checks
             // literals (non-literal lanes store to an unused byte past the window)
             win[(live && !ism) ? d - base : W + 24] = (uint8_t)t;
+            // ---- matches: which in-sub-batch lanes each match's source needs ----
+            // Bit r of the bitmap bm marks an item starting at D + r.  The lane owning
+            // byte D + r is sub0 + (#starts at or before r) - 1; a match needs the lanes owning
+            // [max(s, D), send): the contiguous lane range [la, lb].
+            const uint32_t rs = d - D;  // < kSubMax for `in` lanes
+            bm[lane] = 0;
+            if (in && len) __hip_atomic_fetch_or(&bm[rs >> 5], 1u << (rs & 31), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            // other lanes' ORs land in this lane's word: a compiler barrier so the read is
+            // not folded into the lane's own store (the wave's LDS ops run in issue order)
+            asm volatile("" ::: "memory");
+            const uint32_t bw = bm[lane];
+            const uint32_t bpc = __builtin_popcount(bw);
+            const uint32_t bex = wave_incl_scan(bpc) - bpc;  // starts in words below `lane`
+            const uint32_t send = (s + len < d) ? s + len : d;
+            const bool dep = in && ism && send > D;
+            const uint32_t qa = (dep && s > D) ? s - D : 0u, qb = dep ? send - 1 - D : 0u;
+            // lanes below sub0 (earlier sub-batches) own nothing here; every later valid lane
+            // has len > 0, so the k-th start belongs to lane sub0 + k
+            const uint32_t la = sub0 + owner_of(bm, bex, qa), lb = sub0 + owner_of(bm, bex, qb);
+            const uint64_t need = dep ? ((~0ull << la) & (~0ull >> (63 - lb))) : 0ull;
             // ---- matches: copy in sub-rounds ----
             bool done = !(live && ism && !bad);
-            const uint32_t send = (s + len < d) ? s + len : d;
-            const uint32_t end = d + len;
             const uint32_t n16 = len < 16 ? len : 16;
             Copy16 cp;
             cp.prep(d - base, off, n16);
             uint64_t pend = __ballot(!done);
             while (pend) {
-                // the first three pending matches bound three gaps whose bytes are all final
-                const uint32_t u0 = (uint32_t)__builtin_ctzll(pend);
-                const uint64_t p1 = pend & (pend - 1), p2 = p1 & (p1 - 1);
-                const uint32_t u1 = ff1_or(p1, u0), u2 = ff1_or(p2, u0);
-                const uint32_t d0 = __builtin_amdgcn_readlane(d, u0), e0 = __builtin_amdgcn_readlane(end, u0);
-                const uint32_t d1r = __builtin_amdgcn_readlane(d, u1), e1 = __builtin_amdgcn_readlane(end, u1);
-                const uint32_t d2r = __builtin_amdgcn_readlane(d, u2);
-                const uint32_t d1 = p1 ? d1r : 0xffffffffu, d2 = p2 ? d2r : 0xffffffffu;
-                const bool ready = !done & ((send <= d0) | ((s >= e0) & (send <= d1)) | ((s >= e1) & (send <= d2)));
+                // exact: every byte of the source is final once none of the lanes owning it is pending
+                const bool ready = !done & ((need & pend) == 0);
                 if (ready && !spec) cp.run_sel(win, far, fy);
                 if (__ballot(ready && spec)) {
                     if (ready && spec) {
@@ -632,6 +657,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             if (__ballot(err)) { more = false; complete = false; }
         }
         if (__ballot(err)) break;
+        dma4(src + tokp, lds_addr(bm));  // tokens of batch bt+4 into the slot bt used (bitmap done)
         asm volatile("s_waitcnt vmcnt(" QLZX_STR(QLZX_K2_VMWAIT) ")" ::: "memory");  // DMAs of iterations <= bt-3 landed
         PROF_MARK(4);  // 4: waiting for prefetch
     }
