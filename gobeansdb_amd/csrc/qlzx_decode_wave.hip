@@ -621,11 +621,12 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             Copy16 cp;
             cp.prep(d - base, off, n16);
             uint64_t pend = __ballot(!done);
+            const bool spec_any = __ballot(!done && spec) != 0;  // rare: skip its test per sub-round
             while (pend) {
                 // exact: every byte of the source is final once none of the lanes owning it is pending
                 const bool ready = !done & ((need & pend) == 0);
                 if (ready && !spec) cp.run_sel(win, far, fy);
-                if (__ballot(ready && spec)) {
+                if (spec_any && __ballot(ready && spec)) {
                     if (ready && spec) {
                         if (far || (off < 16 && off < len)) {
                             // byte by byte, in order (short-period overlap, or a source in HBM)
