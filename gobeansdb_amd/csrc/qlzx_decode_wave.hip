@@ -81,7 +81,98 @@ inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
     const uint32_t md = max_dsize > QLZX_FAST_MAX_DSIZE ? QLZX_FAST_MAX_DSIZE : max_dsize;
     const uint32_t c = n < kChunkBlocks ? (n ? n : 1) : kChunkBlocks;
     return (((size_t)c * sizeof(BlkInfo) + 255) & ~(size_t)255) +
-           ((((size_t)c * groups_max(md) * sizeof(GroupRec)) + 255) & ~(size_t)255) + 256;
+           ((((size_t)c * groups_max(md) * sizeof(GroupRec)) + 255) & ~(size_t)255) +
+           ((((size_t)n * sizeof(uint32_t)) + 255) & ~(size_t)255) +              // block order, whole call
+           (((((size_t)n + c - 1) / c * 1024) + 255) & ~(size_t)255) + 256;       // order aux per chunk
+}
+
+// ---------------------------------------------------------- block order ----
+// K1 runs one lane per block, so a wave lasts as long as its longest stream: with mixed
+// 4-64 KiB values (c4, c5) most lanes would idle behind one 64 KiB block.  Two small
+// kernels list the chunk's blocks by compressed size, largest first (counting sort on
+// len / 512), and K1 and K2 take their blocks from that list.  Order within a class is
+// arbitrary: every per-block output is indexed by the block, not by its place in the list.
+// Mixed c5 values: 260 -> 430 GiB/s; uniform c2: unchanged.
+// aux (zeroed before k_order_count): [0,128) class counts, [128,256) class cursors.
+// One-wave workgroups (16 blocks per lane): they fit beside a resident K2 chunk, whose waves
+// fill the CUs; a 1024-thread workgroup waited for a whole CU to drain, which serialised K1
+// behind K2 and cost more than the ordering gained.
+constexpr uint32_t kOrderClasses = 128, kOrderWG = 64, kOrderEPT = 16, kOrderPerWG = kOrderWG * kOrderEPT;
+constexpr uint32_t kOrderAux = 2 * kOrderClasses;
+static_assert(kChunkBlocks % kOrderPerWG == 0, "an order workgroup stays inside one chunk");
+__device__ __forceinline__ uint32_t order_class(uint32_t len) {
+    const uint32_t c = len >> 9;
+    return kOrderClasses - 1 - (c < kOrderClasses - 1 ? c : kOrderClasses - 1);
+}
+// Both kernels cover every chunk of the call in one grid (a workgroup's 1024 blocks never
+// straddle chunks: kChunkBlocks is a multiple of 1024), and are launched before the first
+// K1: a kernel queued between two K1s delays K1(c+1) until K2(c) has filled the CUs, and
+// K1 then waits for K2(c) to drain (12 % on c2).
+struct OrderChunk {
+    uint32_t first, count;
+};
+__device__ __forceinline__ OrderChunk order_chunk(uint32_t n, uint32_t chunk, uint32_t &ci) {
+    ci = (blockIdx.x * kOrderPerWG) / chunk;
+    const uint32_t first = ci * chunk;
+    return OrderChunk{first, n - first < chunk ? n - first : chunk};
+}
+__global__ void __launch_bounds__(kOrderWG) k_order_count(const uint32_t *src_len, uint32_t n, uint32_t chunk,
+                                                         uint32_t *aux_all) {
+    __shared__ uint32_t h[kOrderClasses];
+    uint32_t ci;
+    const OrderChunk oc = order_chunk(n, chunk, ci);
+    const uint32_t first = oc.first, count = oc.count;
+    uint32_t *aux = aux_all + ci * kOrderAux;
+    const uint32_t tid = threadIdx.x, i0 = blockIdx.x * kOrderPerWG - first + tid;
+    for (uint32_t k = tid; k < kOrderClasses; k += kOrderWG) h[k] = 0;
+    __syncthreads();
+    uint32_t len[kOrderEPT];
+#pragma unroll
+    for (uint32_t e = 0; e < kOrderEPT; e++) {
+        const uint32_t i = i0 + e * kOrderWG;
+        len[e] = i < count ? src_len[first + i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < kOrderEPT; e++)
+        if (i0 + e * kOrderWG < count) atomicAdd(&h[order_class(len[e])], 1u);
+    __syncthreads();
+    for (uint32_t k = tid; k < kOrderClasses; k += kOrderWG)
+        if (h[k]) atomicAdd(&aux[k], h[k]);
+}
+__global__ void __launch_bounds__(kOrderWG) k_order_scatter(const uint32_t *src_len, uint32_t n, uint32_t chunk,
+                                                           uint32_t *aux_all, uint32_t *list_all) {
+    __shared__ uint32_t start[kOrderClasses], lc[kOrderClasses];
+    uint32_t ci;
+    const OrderChunk oc = order_chunk(n, chunk, ci);
+    const uint32_t first = oc.first, count = oc.count;
+    uint32_t *aux = aux_all + ci * kOrderAux, *list = list_all + first;
+    const uint32_t tid = threadIdx.x, i0 = blockIdx.x * kOrderPerWG - first + tid;
+    for (uint32_t k = tid; k < kOrderClasses; k += kOrderWG) start[k] = aux[k], lc[k] = 0;
+    __syncthreads();
+    if (tid == 0) {  // exclusive scan of the chunk's class counts (128 LDS words)
+        uint32_t acc = 0;
+        for (uint32_t k = 0; k < kOrderClasses; k++) {
+            const uint32_t v = start[k];
+            start[k] = acc;
+            acc += v;
+        }
+    }
+    uint32_t c[kOrderEPT], r[kOrderEPT];
+#pragma unroll
+    for (uint32_t e = 0; e < kOrderEPT; e++) {
+        const uint32_t i = i0 + e * kOrderWG;
+        c[e] = i < count ? order_class(src_len[first + i]) : 0u;
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < kOrderEPT; e++)
+        r[e] = (i0 + e * kOrderWG < count) ? atomicAdd(&lc[c[e]], 1u) : 0u;  // rank in this workgroup's class
+    __syncthreads();
+    for (uint32_t k = tid; k < kOrderClasses; k += kOrderWG)
+        if (lc[k]) start[k] += atomicAdd(&aux[kOrderClasses + k], lc[k]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t e = 0; e < kOrderEPT; e++)
+        if (i0 + e * kOrderWG < count) list[start[c[e]] + r[e]] = i0 + e * kOrderWG;
 }
 
 // ------------------------------------------------------------------ K1 ----
@@ -117,7 +208,8 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
                                                          uint32_t *dsize_out, int32_t *status,
                                                          const uint32_t *crc_state, const uint32_t *crc_expect,
                                                          uint32_t *crc_out, uint32_t first, uint32_t count,
-                                                         BlkInfo *info, GroupRec *recs, uint32_t gmax) {
+                                                         BlkInfo *info, GroupRec *recs, uint32_t gmax,
+                                                         const uint32_t *order) {
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG<CRC> / 64) * kRingWave];
     __shared__ uint32_t tab[CRC ? 8 * 256 : 1];
     if (CRC) {
@@ -126,8 +218,9 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
     }
     const uint32_t lane = threadIdx.x & 63;
     uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWave;
-    const uint32_t li = blockIdx.x * kParseWG<CRC> + threadIdx.x;
-    const bool inrange = li < count;
+    const uint32_t lin = blockIdx.x * kParseWG<CRC> + threadIdx.x;
+    const bool inrange = lin < count;
+    const uint32_t li = (order && inrange) ? order[lin] : lin;  // block of the chunk
     const uint32_t i = first + (inrange ? li : 0);
 
     int st = QLZX_OK;
@@ -473,7 +566,18 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
     const uint32_t dsize = bi.dsize;
     if (bi.kind == kBlkStored) {  // quicklz.c:808-811
         const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
-        for (uint32_t p = lane; p < dsize; p += 64) dst[p] = src[hdr + p];
+        const uint8_t *s = src + hdr;
+        uint32_t p0 = 0;
+        if ((((uintptr_t)dst) & 15u) == 0) {
+            // 16 B per lane: four unaligned dword loads (unaligned access mode, as in far_load20),
+            // one aligned 16-B store; 1 KiB per wave instruction
+            p0 = dsize & ~15u;
+            for (uint32_t p = lane * 16; p < p0; p += 1024) {
+                const uint32_t *q = (const uint32_t *)(s + p);
+                *(uint4 *)(dst + p) = make_uint4(q[0], q[1], q[2], q[3]);
+            }
+        }
+        for (uint32_t p = p0 + lane; p < dsize; p += 64) dst[p] = s[p];
         if (lane == 0) { status[i] = QLZX_OK; if (dsize_out) dsize_out[i] = dsize; }
         return;
     }
@@ -694,6 +798,13 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     const uint32_t chunk = b.n < kChunkBlocks ? b.n : kChunkBlocks;
     const size_t o_rec = ((size_t)chunk * sizeof(BlkInfo) + 255) & ~(size_t)255;
     const size_t one = decode_wave_ws_bytes(b.n, max_dsize);
+    const size_t o_list = o_rec + ((((size_t)chunk * gmax * sizeof(GroupRec)) + 255) & ~(size_t)255);
+    const size_t o_aux = o_list + ((((size_t)b.n * sizeof(uint32_t)) + 255) & ~(size_t)255);
+    static const bool sort_env = [] {  // QLZX_BLOCK_ORDER=0: chunk order (experiments)
+        const char *e = getenv("QLZX_BLOCK_ORDER");
+        return !(e && e[0] == '0');
+    }();
+    const bool sort = sort_env && chunk > 64;
     // two workspace halves when the caller gave room for them: K1 of chunk c+1 runs on a
     // side stream while K2 of chunk c runs on `s` (K1 is latency-bound at low occupancy)
     static const bool overlap_env = [] {  // QLZX_K1_OVERLAP=0: serial K1/K2 (experiments)
@@ -714,29 +825,40 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     }
     const bool crc = crc_state || crc_expect || crc_out;
     if (overlap) (void)hipEventRecord(ev_k2[1], s), (void)hipStreamWaitEvent(side, ev_k2[1], 0);
+    if (sort) {  // block order of every chunk, ahead of the first K1 (workspace half 0)
+        hipStream_t s1 = overlap ? side : s;
+        uint32_t *aux = (uint32_t *)((uint8_t *)ws + o_aux);
+        const uint32_t nch = (b.n + chunk - 1) / chunk;
+        (void)hipMemsetAsync(aux, 0, (size_t)nch * kOrderAux * sizeof(uint32_t), s1);
+        const dim3 g((nch - 1) * (chunk / kOrderPerWG) + (b.n - (nch - 1) * chunk + kOrderPerWG - 1) / kOrderPerWG);
+        hipLaunchKernelGGL(k_order_count, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, chunk, aux);
+        hipLaunchKernelGGL(k_order_scatter, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, chunk, aux,
+                           (uint32_t *)((uint8_t *)ws + o_list));
+    }
     uint32_t c = 0;
     for (uint32_t first = 0; first < b.n; first += chunk, c++) {
         const uint32_t cnt = b.n - first < chunk ? b.n - first : chunk;
         uint8_t *w = (uint8_t *)ws + (overlap ? (c & 1) * one : 0);
         BlkInfo *info = (BlkInfo *)w;
         GroupRec *recs = (GroupRec *)(w + o_rec);
+        uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
         hipStream_t s1 = overlap ? side : s;
         if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
         if (crc)
             hipLaunchKernelGGL(k_dec_parse<true>, dim3((cnt + kParseWG<true> - 1) / kParseWG<true>),
                                dim3(kParseWG<true>), 0, s1, b,
-                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax);
+                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order);
         else
             hipLaunchKernelGGL(k_dec_parse<false>, dim3((cnt + kParseWG<false> - 1) / kParseWG<false>),
                                dim3(kParseWG<false>), 0, s1, b,
-                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax);
+                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order);
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
 #ifndef QLZX_EXP_K2_EXTRA_LDS
 #define QLZX_EXP_K2_EXTRA_LDS 0  // experiments: extra dynamic LDS per WG to lower occupancy
 #endif
         // one kernel for every block size: the LDS window slides over longer blocks
         hipLaunchKernelGGL(k_dec_blocks<kWin>, dim3(cnt), dim3(64), QLZX_EXP_K2_EXTRA_LDS, s, b, dsize, status,
-                           first, cnt, info, recs, gmax, (const uint32_t *)nullptr);
+                           first, cnt, info, recs, gmax, (const uint32_t *)order);
         if (overlap) (void)hipEventRecord(ev_k2[c & 1], s);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;

@@ -224,3 +224,34 @@ def test_multi_chunk_overlap_round_trip(cuda, crc):
     assert torch.equal(out.data[pos], plain.data[pos])
     if crc:
         assert torch.equal(crc_out, batch.crc32(src))
+
+
+def test_mixed_sizes_block_order_round_trip(cuda):
+    """Log-uniform 1-64 KiB text and image-like blocks over two decode chunks: K1 and K2 take
+    their blocks from the size-ordered list (k_order_count / k_order_scatter), so every block's
+    output must still land at its own offset.  Compared by per-block CRC32 of output vs plain."""
+    import numpy as np
+    import torch
+    from gobeansdb_amd import batch
+    n = 131072 + 3000
+    rng = np.random.default_rng(5)
+    lens = np.exp(rng.uniform(np.log(1024), np.log(65536), n)).astype(np.int64)
+    n_img = n * 3 // 10    # image-like blocks: mostly stored in the mix
+    parts = [batch.synth("text", 91, lens[n_img:].tolist()), batch.synth("image", 92, lens[:n_img].tolist())]
+    comps = []
+    for plain in parts:
+        comp, cs, st, _ = batch.compress(plain, max_len=65536)
+        assert int((st != 0).sum()) == 0
+        comps.append((comp, cs))
+    perm = torch.from_numpy(rng.permutation(n)).cuda()
+    data = torch.cat([comps[0][0].data, comps[1][0].data])
+    off = torch.cat([comps[0][0].off, comps[1][0].off + comps[0][0].data.numel()])
+    src = batch.BlockBatch(data, off[perm], torch.cat([comps[0][1], comps[1][1]])[perm])
+    plen = torch.cat([parts[0].length, parts[1].length])[perm]
+    out = batch.BlockBatch.empty_for(plen.cpu().numpy().astype(np.int64).tolist())
+    expect = torch.cat([batch.crc32(parts[0]), batch.crc32(parts[1])])[perm]
+    dsz, st2, _ = batch.decompress(src, out, max_dsize=65536)
+    torch.cuda.synchronize()
+    assert int((st2 != 0).sum()) == 0
+    assert torch.equal(dsz, plen)
+    assert torch.equal(batch.crc32(out), expect)
