@@ -479,21 +479,14 @@ struct Copy16 {
         }
         mk[0] &= 0xffffffffu << (8 * lo);
     }
-    // as run(), but lanes with `far` set take their source dwords from y[] (HBM)
-    __device__ __forceinline__ void run_sel(uint8_t *out, bool far, const uint32_t y[5]) const {
-        const uint32_t *x = (const uint32_t *)(out + (far ? 0 : xa));
-        const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4], x5 = x[5];
-        const uint32_t v0 = far ? y[0] : __builtin_amdgcn_alignbyte(x1, x0, sh);
-        const uint32_t v1 = far ? y[1] : __builtin_amdgcn_alignbyte(x2, x1, sh);
-        const uint32_t v2 = far ? y[2] : __builtin_amdgcn_alignbyte(x3, x2, sh);
-        const uint32_t v3 = far ? y[3] : __builtin_amdgcn_alignbyte(x4, x3, sh);
-        const uint32_t v4 = far ? y[4] : __builtin_amdgcn_alignbyte(x5, x4, sh);
+    // source dwords already in registers (far matches: y[] from HBM)
+    __device__ __forceinline__ void run_y(uint8_t *out, const uint32_t y[5]) const {
         uint32_t *dw = (uint32_t *)(out + qa);
-        lds_mskor<0>(dw, mk[0], v0 & mk[0]);
-        lds_mskor<4>(dw, mk[1], v1 & mk[1]);
-        lds_mskor<8>(dw, mk[2], v2 & mk[2]);
-        lds_mskor<12>(dw, mk[3], v3 & mk[3]);
-        lds_mskor<16>(dw, mk[4], v4 & mk[4]);
+        lds_mskor<0>(dw, mk[0], y[0] & mk[0]);
+        lds_mskor<4>(dw, mk[1], y[1] & mk[1]);
+        lds_mskor<8>(dw, mk[2], y[2] & mk[2]);
+        lds_mskor<12>(dw, mk[3], y[3] & mk[3]);
+        lds_mskor<16>(dw, mk[4], y[4] & mk[4]);
     }
     __device__ __forceinline__ void run(uint8_t *out) const {
         const uint32_t *x = (const uint32_t *)(out + xa);
@@ -724,12 +717,21 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             const uint32_t n16 = len < 16 ? len : 16;
             Copy16 cp;
             cp.prep(d - base, off, n16);
+            // far matches (source in HBM, below the window) depend on no lane of this batch:
+            // copy them before the sub-rounds, so the loop needs no source select
+            {
+                const bool fc = !done && far && !spec;
+                if (__ballot(fc)) {
+                    if (fc) cp.run_y(win, fy);
+                }
+                done = done || fc;
+            }
             uint64_t pend = __ballot(!done);
             const bool spec_any = __ballot(!done && spec) != 0;  // rare: skip its test per sub-round
             while (pend) {
                 // exact: every byte of the source is final once none of the lanes owning it is pending
                 const bool ready = !done & ((need & pend) == 0);
-                if (ready && !spec) cp.run_sel(win, far, fy);
+                if (ready && !spec) cp.run(win);
                 if (spec_any && __ballot(ready && spec)) {
                     if (ready && spec) {
                         if (far || (off < 16 && off < len)) {
@@ -749,7 +751,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                     }
                 }
 #ifdef QLZX_EXP_ONESUB  // experiment: every pending match copies in the first sub-round (timing only)
-                if (!ready && !done && !spec) cp.run_sel(win, far, fy);
+                if (!ready && !done && !spec) cp.run(win);
                 done = true;
 #endif
                 done = done || ready;
