@@ -83,73 +83,53 @@ inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
     return (((size_t)c * sizeof(BlkInfo) + 255) & ~(size_t)255) +
            ((((size_t)c * groups_max(md) * sizeof(GroupRec)) + 255) & ~(size_t)255) +
            ((((size_t)n * sizeof(uint32_t)) + 255) & ~(size_t)255) +              // block order, whole call
-           (((((size_t)n + c - 1) / c * 1024) + 255) & ~(size_t)255) + 256;       // order aux per chunk
+           1024 + 256;                                                            // order aux
 }
 
 // ---------------------------------------------------------- block order ----
 // K1 runs one lane per block, so a wave lasts as long as its longest stream: with mixed
 // 4-64 KiB values (c4, c5) most lanes would idle behind one 64 KiB block.  Two small
-// kernels list the chunk's blocks by compressed size, largest first (counting sort on
-// len / 512), and K1 and K2 take their blocks from that list.  Order within a class is
-// arbitrary: every per-block output is indexed by the block, not by its place in the list.
-// Mixed c5 values: 260 -> 430 GiB/s; uniform c2: unchanged.
+// kernels list ALL blocks of the call by compressed size, smallest first (counting sort on
+// len / 512, 128 classes), and the chunks are cut from that list: K1 and K2 of chunk c take
+// blocks list[c * chunk ..] and index their workspace by the place in the chunk.  So a K1
+// wave's lanes have similar lengths, and K1(c+1), whose blocks are at most a class longer,
+// hides under K2(c), whose chunk has as many blocks; the first, exposed K1 parses the
+// smallest blocks.  Order within a class is arbitrary: outputs are indexed by the block.
 // aux (zeroed before k_order_count): [0,128) class counts, [128,256) class cursors.
-// One-wave workgroups (16 blocks per lane): they fit beside a resident K2 chunk, whose waves
-// fill the CUs; a 1024-thread workgroup waited for a whole CU to drain, which serialised K1
-// behind K2 and cost more than the ordering gained.
+// One-wave workgroups (16 blocks per lane), launched before the first K1: a kernel queued
+// between two K1s on the side stream delayed K1(c+1) until K2(c) had filled the CUs, and a
+// 1024-thread workgroup waited for a whole CU to drain; both serialised K1 behind K2.
 constexpr uint32_t kOrderClasses = 128, kOrderWG = 64, kOrderEPT = 16, kOrderPerWG = kOrderWG * kOrderEPT;
 constexpr uint32_t kOrderAux = 2 * kOrderClasses;
-static_assert(kChunkBlocks % kOrderPerWG == 0, "an order workgroup stays inside one chunk");
 __device__ __forceinline__ uint32_t order_class(uint32_t len) {
     const uint32_t c = len >> 9;
-    return kOrderClasses - 1 - (c < kOrderClasses - 1 ? c : kOrderClasses - 1);
+    return c < kOrderClasses - 1 ? c : kOrderClasses - 1;
 }
-// Both kernels cover every chunk of the call in one grid (a workgroup's 1024 blocks never
-// straddle chunks: kChunkBlocks is a multiple of 1024), and are launched before the first
-// K1: a kernel queued between two K1s delays K1(c+1) until K2(c) has filled the CUs, and
-// K1 then waits for K2(c) to drain (12 % on c2).
-struct OrderChunk {
-    uint32_t first, count;
-};
-__device__ __forceinline__ OrderChunk order_chunk(uint32_t n, uint32_t chunk, uint32_t &ci) {
-    ci = (blockIdx.x * kOrderPerWG) / chunk;
-    const uint32_t first = ci * chunk;
-    return OrderChunk{first, n - first < chunk ? n - first : chunk};
-}
-__global__ void __launch_bounds__(kOrderWG) k_order_count(const uint32_t *src_len, uint32_t n, uint32_t chunk,
-                                                         uint32_t *aux_all) {
+__global__ void __launch_bounds__(kOrderWG) k_order_count(const uint32_t *src_len, uint32_t n, uint32_t *aux) {
     __shared__ uint32_t h[kOrderClasses];
-    uint32_t ci;
-    const OrderChunk oc = order_chunk(n, chunk, ci);
-    const uint32_t first = oc.first, count = oc.count;
-    uint32_t *aux = aux_all + ci * kOrderAux;
-    const uint32_t tid = threadIdx.x, i0 = blockIdx.x * kOrderPerWG - first + tid;
+    const uint32_t tid = threadIdx.x, i0 = blockIdx.x * kOrderPerWG + tid;
     for (uint32_t k = tid; k < kOrderClasses; k += kOrderWG) h[k] = 0;
     __syncthreads();
     uint32_t len[kOrderEPT];
 #pragma unroll
     for (uint32_t e = 0; e < kOrderEPT; e++) {
         const uint32_t i = i0 + e * kOrderWG;
-        len[e] = i < count ? src_len[first + i] : 0u;
+        len[e] = i < n ? src_len[i] : 0u;
     }
 #pragma unroll
     for (uint32_t e = 0; e < kOrderEPT; e++)
-        if (i0 + e * kOrderWG < count) atomicAdd(&h[order_class(len[e])], 1u);
+        if (i0 + e * kOrderWG < n) atomicAdd(&h[order_class(len[e])], 1u);
     __syncthreads();
     for (uint32_t k = tid; k < kOrderClasses; k += kOrderWG)
         if (h[k]) atomicAdd(&aux[k], h[k]);
 }
-__global__ void __launch_bounds__(kOrderWG) k_order_scatter(const uint32_t *src_len, uint32_t n, uint32_t chunk,
-                                                           uint32_t *aux_all, uint32_t *list_all) {
+__global__ void __launch_bounds__(kOrderWG) k_order_scatter(const uint32_t *src_len, uint32_t n, uint32_t *aux,
+                                                           uint32_t *list) {
     __shared__ uint32_t start[kOrderClasses], lc[kOrderClasses];
-    uint32_t ci;
-    const OrderChunk oc = order_chunk(n, chunk, ci);
-    const uint32_t first = oc.first, count = oc.count;
-    uint32_t *aux = aux_all + ci * kOrderAux, *list = list_all + first;
-    const uint32_t tid = threadIdx.x, i0 = blockIdx.x * kOrderPerWG - first + tid;
+    const uint32_t tid = threadIdx.x, i0 = blockIdx.x * kOrderPerWG + tid;
     for (uint32_t k = tid; k < kOrderClasses; k += kOrderWG) start[k] = aux[k], lc[k] = 0;
     __syncthreads();
-    if (tid == 0) {  // exclusive scan of the chunk's class counts (128 LDS words)
+    if (tid == 0) {  // exclusive scan of the class counts (128 LDS words)
         uint32_t acc = 0;
         for (uint32_t k = 0; k < kOrderClasses; k++) {
             const uint32_t v = start[k];
@@ -161,18 +141,18 @@ __global__ void __launch_bounds__(kOrderWG) k_order_scatter(const uint32_t *src_
 #pragma unroll
     for (uint32_t e = 0; e < kOrderEPT; e++) {
         const uint32_t i = i0 + e * kOrderWG;
-        c[e] = i < count ? order_class(src_len[first + i]) : 0u;
+        c[e] = i < n ? order_class(src_len[i]) : 0u;
     }
 #pragma unroll
     for (uint32_t e = 0; e < kOrderEPT; e++)
-        r[e] = (i0 + e * kOrderWG < count) ? atomicAdd(&lc[c[e]], 1u) : 0u;  // rank in this workgroup's class
+        r[e] = (i0 + e * kOrderWG < n) ? atomicAdd(&lc[c[e]], 1u) : 0u;  // rank in this workgroup's class
     __syncthreads();
     for (uint32_t k = tid; k < kOrderClasses; k += kOrderWG)
         if (lc[k]) start[k] += atomicAdd(&aux[kOrderClasses + k], lc[k]);
     __syncthreads();
 #pragma unroll
     for (uint32_t e = 0; e < kOrderEPT; e++)
-        if (i0 + e * kOrderWG < count) list[start[c[e]] + r[e]] = i0 + e * kOrderWG;
+        if (i0 + e * kOrderWG < n) list[start[c[e]] + r[e]] = i0 + e * kOrderWG;
 }
 
 // ------------------------------------------------------------------ K1 ----
@@ -220,8 +200,8 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
     uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWave;
     const uint32_t lin = blockIdx.x * kParseWG<CRC> + threadIdx.x;
     const bool inrange = lin < count;
-    const uint32_t li = (order && inrange) ? order[lin] : lin;  // block of the chunk
-    const uint32_t i = first + (inrange ? li : 0);
+    // block: the lin-th of the chunk's list (or of the call, in order); workspace slot: lin
+    const uint32_t i = inrange ? (order ? order[lin] : first + lin) : first;
 
     int st = QLZX_OK;
     uint32_t kind = kBlkSkip, csize = 0, dsize = 0, hdr = 0, len = 0;
@@ -259,7 +239,7 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
 
     // parse state
     uint32_t ip = hdr, g = 0, k = 31, cw = 0, m = 0, ra = 0, rb = 0, rec_ip = 0;
-    GroupRec *myrec = recs + (size_t)(inrange ? li : 0) * gmax;
+    GroupRec *myrec = recs + (size_t)(inrange ? lin : 0) * gmax;
     uint32_t crc = (CRC && inrange && crc_state) ? crc_state[i] : 0xffffffffu;
     bool done_parse = !parsing;
 
@@ -372,7 +352,7 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
         bi.ngroups = g;
         bi.nitems = (g - 1) * 31 + (k > 31 ? 31 : k);
     }
-    info[li] = bi;
+    info[lin] = bi;
 }
 
 // ------------------------------------------------------------------ K2 ----
@@ -549,10 +529,10 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
     static_assert(W % 2048 == 0 && W >= 2048, "window: a multiple of 2 KiB (slides by W/2)");
     __shared__ __attribute__((aligned(16))) K2Lds<W> L;
     const uint32_t lane = threadIdx.x;
-    if (blockIdx.x >= count) return;
-    const uint32_t li = list ? list[blockIdx.x] : blockIdx.x;  // block of the chunk (size-class list)
-    const uint32_t i = first + li;
-    const BlkInfo bi = info[li];
+    const uint32_t bx = blockIdx.x;  // workspace slot
+    if (bx >= count) return;
+    const uint32_t i = list ? list[bx] : first + bx;  // block
+    const BlkInfo bi = info[bx];
     if (bi.kind == kBlkSkip) return;
     const uint8_t *src = b.src + b.src_off[i];
     uint8_t *dst = b.dst + b.dst_off[i];
@@ -575,7 +555,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
         return;
     }
     uint8_t *win = L.win;
-    const GroupRec *rb = recs + (size_t)li * gmax;
+    const GroupRec *rb = recs + (size_t)bx * gmax;
     const uint32_t nitems = bi.nitems, ngroups = bi.ngroups;
     const uint32_t csize = b.src_len[i];
     const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
@@ -827,14 +807,13 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     }
     const bool crc = crc_state || crc_expect || crc_out;
     if (overlap) (void)hipEventRecord(ev_k2[1], s), (void)hipStreamWaitEvent(side, ev_k2[1], 0);
-    if (sort) {  // block order of every chunk, ahead of the first K1 (workspace half 0)
+    if (sort) {  // block order of the whole call, ahead of the first K1 (workspace half 0)
         hipStream_t s1 = overlap ? side : s;
         uint32_t *aux = (uint32_t *)((uint8_t *)ws + o_aux);
-        const uint32_t nch = (b.n + chunk - 1) / chunk;
-        (void)hipMemsetAsync(aux, 0, (size_t)nch * kOrderAux * sizeof(uint32_t), s1);
-        const dim3 g((nch - 1) * (chunk / kOrderPerWG) + (b.n - (nch - 1) * chunk + kOrderPerWG - 1) / kOrderPerWG);
-        hipLaunchKernelGGL(k_order_count, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, chunk, aux);
-        hipLaunchKernelGGL(k_order_scatter, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, chunk, aux,
+        (void)hipMemsetAsync(aux, 0, kOrderAux * sizeof(uint32_t), s1);
+        const dim3 g((b.n + kOrderPerWG - 1) / kOrderPerWG);
+        hipLaunchKernelGGL(k_order_count, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, aux);
+        hipLaunchKernelGGL(k_order_scatter, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, aux,
                            (uint32_t *)((uint8_t *)ws + o_list));
     }
     uint32_t c = 0;
