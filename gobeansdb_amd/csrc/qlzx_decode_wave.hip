@@ -63,14 +63,17 @@ constexpr uint32_t kRingWave = kRingSlots * kRoundBytes * 64;  // 16 KiB per wav
 #define QLZX_K2_WIN 4096
 #endif
 constexpr uint32_t kWin = QLZX_K2_WIN;          // K2 LDS history window (bytes)
-constexpr uint32_t kK2Slack = 3;              // K2: iterations a prefetch DMA has to land
-constexpr uint32_t kTokAhead = kK2Slack + 1;   // tokens of batch bt + 4 issued in iteration bt
-constexpr uint32_t kRecAhead = 2 * kTokAhead;  // records of batch bt + 8 issued in iteration bt
-constexpr uint32_t kTokSlots = kTokAhead;      // batches bt .. bt+3 (bt+4 reuses bt's slot)
-constexpr uint32_t kRecSlots = kTokAhead + 1;  // batches bt+4 .. bt+8
+#ifndef QLZX_K2_SLACK
+#define QLZX_K2_SLACK 3
+#endif
+constexpr uint32_t kK2Slack = QLZX_K2_SLACK;  // K2: iterations a prefetch DMA has to land
+constexpr uint32_t kTokAhead = kK2Slack + 1;   // tokens of batch bt + kTokAhead issued in iteration bt
+constexpr uint32_t kRecAhead = 2 * kTokAhead;  // records of batch bt + kRecAhead issued in iteration bt
+constexpr uint32_t kTokSlots = kTokAhead;      // batches bt .. bt+kTokAhead-1 (bt+kTokAhead reuses bt's slot)
+constexpr uint32_t kRecSlots = kTokAhead + 1;  // batches bt+kTokAhead .. bt+kRecAhead
 constexpr uint32_t kSubMax = 64 * 32;          // K2 sub-batch output bound: the 64-word item-start bitmap
 #ifndef QLZX_K2_VMWAIT
-#define QLZX_K2_VMWAIT 6  // = 2 * kK2Slack; experiments only: other values break the prefetch invariant
+#define QLZX_K2_VMWAIT 6  // = 2 * QLZX_K2_SLACK (set both together); other values break the prefetch invariant
 #endif
 
 __host__ __device__ inline uint32_t groups_max(uint32_t max_dsize) { return max_dsize / 31u + 2u; }
@@ -381,9 +384,11 @@ struct K2Lds {
 
 // Every K2 iteration issues exactly 2 DMA instructions (1 token dword + 1
 // record), with dummy addresses for lanes/batches past the end, so that
-// "s_waitcnt vmcnt(6)" at the end of iteration bt means "everything issued up
-// to iteration bt-3 has landed".  Iteration bt issues the tokens of bt+4 and
-// the records of bt+8, so both have three whole iterations to arrive.
+// "s_waitcnt vmcnt(2 * kK2Slack)" at the end of iteration bt means "everything
+// issued up to iteration bt - kK2Slack has landed".  Iteration bt issues the
+// tokens of bt + kTokAhead and the records of bt + kRecAhead, so both have
+// kK2Slack whole iterations to arrive.  Slack 2 saves 320 B of LDS per wave
+// (29 -> 31 waves/CU) but measured within noise of slack 3 (c2 and c5), so 3 stays.
 template <bool DMA = true>
 __device__ __forceinline__ void issue_rec(GroupRec *slot, const GroupRec *rb, uint32_t g0, uint32_t ngroups,
                                           uint32_t lane) {
