@@ -40,7 +40,7 @@ def build(force: bool = False, verbose: bool = False, profile: bool = False) -> 
     if force or _stale():
         _compile(OUT, [], verbose)
     if profile:
-        _compile(PROF_OUT, ["-DQLZX_PROFILE"], verbose)
+        _compile(PROF_OUT, ["-DQLZX_PROFILE", "-DQLZX_SP_WAVES_PER_EU=1"], verbose)
     return OUT
 
 

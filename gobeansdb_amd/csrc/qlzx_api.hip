@@ -14,6 +14,7 @@
 #include "qlzx_tables.hip"
 #include "qlzx_crc.hip"
 #include "qlzx_decode_wave.hip"
+#include "qlzx_decode_split.hip"
 #include "qlzx_decode_lane8.hip"
 #include "qlzx_encode_lane.hip"
 #include "qlzx_encode_wg.hip"

@@ -626,7 +626,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             const bool act = lane >= lo_lane;
             const uint32_t len = act ? len0 : 0u;
             uint32_t incl = wave_incl_scan(len);
-            uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+            uint32_t total = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(incl, 63));
             if (D + total > base + W && D - base >= W / 2) {
                 // slide: flush win[0, W/2) to HBM, move the rest down, base += W/2
                 for (uint32_t q = lane * 16; q < W / 2; q += 1024) {
@@ -636,7 +636,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                 }
                 for (uint32_t q = lane * 16; q < D - base - W / 2; q += 1024)
                     *(uint4 *)(win + q) = *(const uint4 *)(win + W / 2 + q);
-                base += W / 2;
+                base = __builtin_amdgcn_readfirstlane(base + W / 2);
             }
             const uint32_t d = D + incl - len;
             // this sub-batch: the active lanes whose output fits the window (a prefix)
@@ -645,7 +645,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             const uint32_t cut = outm ? (uint32_t)__builtin_ctzll(outm) : 64u;
             const bool in = act && lane < cut;
             more = cut < 64;
-            lo_lane = cut;
+            lo_lane = __builtin_amdgcn_readfirstlane(cut);
             const uint32_t stotal = cut < 64 ? __builtin_amdgcn_readlane(incl - len, cut) : total;
             // far sources (below the window, already in HBM): load them first, use them in the first sub-round
             const uint32_t s = d - off;
@@ -745,7 +745,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                 pend = __ballot(!done);
             }
             PROF_MARK(3);  // 3: match sub-rounds
-            D += stotal;
+            D = __builtin_amdgcn_readfirstlane(D + stotal);
             if (__ballot(err)) { more = false; complete = false; }
         }
         if (__ballot(err)) break;
@@ -774,82 +774,6 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
         status[i] = QLZX_OK;
         if (dsize_out) dsize_out[i] = dsize;
     }
-}
-
-inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uint32_t *dsize,
-                              int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
-                              uint32_t *crc_out, uint32_t max_dsize, void *ws, size_t ws_bytes,
-                              hipStream_t s) {
-    const uint32_t md = max_dsize > QLZX_FAST_MAX_DSIZE ? QLZX_FAST_MAX_DSIZE : max_dsize;
-    const uint32_t gmax = groups_max(md);
-    const uint32_t chunk = b.n < kChunkBlocks ? b.n : kChunkBlocks;
-    const size_t o_rec = ((size_t)chunk * sizeof(BlkInfo) + 255) & ~(size_t)255;
-    const size_t one = decode_wave_ws_bytes(b.n, max_dsize);
-    const size_t o_list = o_rec + ((((size_t)chunk * gmax * sizeof(GroupRec)) + 255) & ~(size_t)255);
-    const size_t o_aux = o_list + ((((size_t)b.n * sizeof(uint32_t)) + 255) & ~(size_t)255);
-    static const bool sort_env = [] {  // QLZX_BLOCK_ORDER=0: chunk order (experiments)
-        const char *e = getenv("QLZX_BLOCK_ORDER");
-        return !(e && e[0] == '0');
-    }();
-    const bool sort = sort_env && chunk > 64;
-    // two workspace halves when the caller gave room for them: K1 of chunk c+1 runs on a
-    // side stream while K2 of chunk c runs on `s` (K1 is latency-bound at low occupancy)
-    static const bool overlap_env = [] {  // QLZX_K1_OVERLAP=0: serial K1/K2 (experiments)
-        const char *e = getenv("QLZX_K1_OVERLAP");
-        return !(e && e[0] == '0');
-    }();
-    const bool overlap = overlap_env && ws_bytes >= 2 * one && b.n > chunk;
-    // per host thread (the batch API is re-entrant like the reference); the side stream
-    // belongs to the device that was current at the thread's first overlapped call
-    thread_local hipStream_t side = nullptr;
-    thread_local hipEvent_t ev_k1[2], ev_k2[2];
-    if (overlap && !side) {
-        if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) return (int)hipErrorUnknown;
-        for (int j = 0; j < 2; j++) {
-            (void)hipEventCreateWithFlags(&ev_k1[j], hipEventDisableTiming);
-            (void)hipEventCreateWithFlags(&ev_k2[j], hipEventDisableTiming);
-        }
-    }
-    const bool crc = crc_state || crc_expect || crc_out;
-    if (overlap) (void)hipEventRecord(ev_k2[1], s), (void)hipStreamWaitEvent(side, ev_k2[1], 0);
-    if (sort) {  // block order of the whole call, ahead of the first K1 (workspace half 0)
-        hipStream_t s1 = overlap ? side : s;
-        uint32_t *aux = (uint32_t *)((uint8_t *)ws + o_aux);
-        (void)hipMemsetAsync(aux, 0, kOrderAux * sizeof(uint32_t), s1);
-        const dim3 g((b.n + kOrderPerWG - 1) / kOrderPerWG);
-        hipLaunchKernelGGL(k_order_count, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, aux);
-        hipLaunchKernelGGL(k_order_scatter, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, aux,
-                           (uint32_t *)((uint8_t *)ws + o_list));
-    }
-    uint32_t c = 0;
-    for (uint32_t first = 0; first < b.n; first += chunk, c++) {
-        const uint32_t cnt = b.n - first < chunk ? b.n - first : chunk;
-        uint8_t *w = (uint8_t *)ws + (overlap ? (c & 1) * one : 0);
-        BlkInfo *info = (BlkInfo *)w;
-        GroupRec *recs = (GroupRec *)(w + o_rec);
-        uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
-        hipStream_t s1 = overlap ? side : s;
-        if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
-        if (crc)
-            hipLaunchKernelGGL(k_dec_parse<true>, dim3((cnt + kParseWG<true> - 1) / kParseWG<true>),
-                               dim3(kParseWG<true>), 0, s1, b,
-                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order);
-        else
-            hipLaunchKernelGGL(k_dec_parse<false>, dim3((cnt + kParseWG<false> - 1) / kParseWG<false>),
-                               dim3(kParseWG<false>), 0, s1, b,
-                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order);
-        if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
-#ifndef QLZX_EXP_K2_EXTRA_LDS
-#define QLZX_EXP_K2_EXTRA_LDS 0  // experiments: extra dynamic LDS per WG to lower occupancy
-#endif
-        // one kernel for every block size: the LDS window slides over longer blocks
-        hipLaunchKernelGGL(k_dec_blocks<kWin>, dim3(cnt), dim3(64), QLZX_EXP_K2_EXTRA_LDS, s, b, dsize, status,
-                           first, cnt, info, recs, gmax, (const uint32_t *)order);
-        if (overlap) (void)hipEventRecord(ev_k2[c & 1], s);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return (int)e;
-    }
-    return 0;
 }
 
 }  // namespace qlzx

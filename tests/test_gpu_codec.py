@@ -57,7 +57,7 @@ def test_compress_golden_bit_exact(cuda, golden):
 
 # general=True: every block through the general lane-per-block kernel (values over 64 KiB)
 @pytest.mark.parametrize("general", [False, True])
-def test_decompress_golden(cuda, golden, general):
+def test_decompress_golden(cuda, golden, general, k2):
     vs = golden.vectors
     outs, st, crc = _gpu_decompress([golden.get(v["c_out"]) for v in vs], want_crc=True, general=general)
     assert (st == 0).all(), [(v["name"], s) for v, s in zip(vs, st) if s]
@@ -108,7 +108,7 @@ def test_cdecompress_safe_errors(cuda, golden):
 
 
 @pytest.mark.parametrize("general", [False, True])
-def test_corrupt_status_matches_oracle(cuda, golden, general):
+def test_corrupt_status_matches_oracle(cuda, golden, general, k2):
     rng = np.random.default_rng(5)
     base = [golden.get(v["c_out"]) for v in golden.vectors if v["cls"] in ("text", "runs", "kat") and v["n"] >= 100]
     cases = []
@@ -166,7 +166,7 @@ def test_go_compat_compress(cuda):
 
 
 @pytest.mark.parametrize("general", [False, True])
-def test_record_fused_crc_verify(cuda, golden, general):
+def test_record_fused_crc_verify(cuda, golden, general, k2):
     """store/datafile.go:161-168: CRC over header[4:24] ‖ key ‖ value, fused with decompress."""
     import struct
     import torch
@@ -196,7 +196,7 @@ def test_record_fused_crc_verify(cuda, golden, general):
 
 
 @pytest.mark.parametrize("crc", [False, True])
-def test_multi_chunk_overlap_round_trip(cuda, crc):
+def test_multi_chunk_overlap_round_trip(cuda, crc, k2):
     """More blocks than one decode chunk (131072): K1 of chunk c+1 runs on the side stream while K2
     of chunk c runs (two workspace halves).  Every block must round-trip, and with crc the fused
     record CRC must equal a separate CRC pass over the compressed values."""
@@ -226,7 +226,7 @@ def test_multi_chunk_overlap_round_trip(cuda, crc):
         assert torch.equal(crc_out, batch.crc32(src))
 
 
-def test_mixed_sizes_block_order_round_trip(cuda):
+def test_mixed_sizes_block_order_round_trip(cuda, k2):
     """Log-uniform 1-64 KiB text and image-like blocks over two decode chunks: K1 and K2 take
     their blocks from the size-ordered list (k_order_count / k_order_scatter), so every block's
     output must still land at its own offset.  Compared by per-block CRC32 of output vs plain."""

@@ -29,7 +29,7 @@ out = batch.BlockBatch.empty_for([bs] * n, device=dev)
 ws = batch.Workspace(dev)
 batch.decompress(src, out, max_dsize=bs, workspace=ws)
 torch.cuda.synchronize()
-prof = torch.zeros(16, dtype=torch.int64, device=dev)
+prof = torch.zeros(32, dtype=torch.int64, device=dev)
 assert L.qlzx_profile_set(prof.data_ptr()) == 0
 t0 = time.time()
 dsz, st, _ = batch.decompress(src, out, max_dsize=bs, workspace=ws)
@@ -51,3 +51,10 @@ print("K1 parse iterations per wave-round: %.1f, active lanes per iteration (lan
 names2 = ["state reads", "prefetch issue", "decode+scan+checks", "sub-rounds", "wait prefetch", "write-out"]
 print("K2 per batch (cycles):", {nm: round(p[8 + j] / batches) for j, nm in enumerate(names2)})
 print("K2 per block total (cycles):", round(p[8:14].sum() / n))
+names3 = ["wait DMA", "item decode", "IP scan+checks+writes", "MP steps", "prefetch issue"]
+print("K2 split per IP batch (cycles):", {nm: round(p[16 + j] / batches) for j, nm in enumerate(names3)})
+print("K2 split per block total (cycles):", round(p[16:21].sum() / n))
+names4 = ["coverage", "readiness", "far", "copy", "spec", "carry"]
+steps = max(p[30], 1)
+print("K2 split MP per step (cycles):", {nm: round(p[24 + j] / steps) for j, nm in enumerate(names4)})
+print("K2 split MP steps per block: %.1f, far-load steps per block: %.1f" % (p[30] / n, p[31] / n))
