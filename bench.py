@@ -37,7 +37,15 @@ def log(*a):
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks (one per GPU); > 1 without a torch.distributed.run environment "
+                        "starts torch.distributed.run with that many ranks as a child process")
+    p.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
+                   help="c2: decompress 1 M x 16 KiB text (BASELINE metric); c3: compress 1 M x 64 KiB "
+                        "image-like (= --mode compress); c5: 400 GiB of mixed values (tools/bench_c5.py)")
+    p.add_argument("--standin", choices=["cpu"], default=None,
+                   help="launcher test only: a CPU stand-in step on gloo instead of the GPU codec "
+                        "(no measurement; used by tests/test_bench_launcher.py)")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--blocks", type=int, default=1 << 20, help="blocks per GPU")
@@ -56,11 +64,41 @@ def parse():
     return p.parse_args()
 
 
+def launch(n: int, argv: list[str]) -> int:
+    """Run this script under torch.distributed.run with n ranks as a CHILD process (the parent
+    has not touched the GPU and never execs), relay its output, return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    log(f"launching {n} ranks: {' '.join(cmd[1:])}")
+    try:
+        return subprocess.run(cmd).returncode
+    except OSError as e:
+        log(f"launch failed: {e}")
+        return 1
+
+
 def main():
     args = parse()
-    from gobeansdb_amd import _lib, batch, shard
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args.gpus, sys.argv[1:]))
+    from gobeansdb_amd import shard
     rank, world, local = shard.env_rank()
+    if world != args.gpus:
+        log(f"WORLD_SIZE {world} != --gpus {args.gpus}: refusing to report a mislabelled line")
+        sys.exit(2)
+    if args.standin:
+        return bench_standin(args, rank, world)
+    if args.config == "c5":
+        return bench_c5(args)
+    if args.config == "c3":
+        args.mode = "compress"
+    from gobeansdb_amd import _lib, batch
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -164,7 +202,11 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline(kind, bs, args.cpu_seconds)
+        # the first 256 GPU-compressed blocks of rank 0 = blocks 0..255 of the CPU leg's sample
+        ns = min(256, uniq)
+        cb = cbuf[: int(coff[ns - 1]) + int(cs_all[ns - 1])].cpu().numpy()
+        gpu_comp = [cb[int(coff[j]): int(coff[j]) + int(cs_all[j])].tobytes() for j in range(ns)]
+        cpu = cpu_baseline(kind, bs, args.cpu_seconds, gpu_comp=gpu_comp)
 
     if rank == 0:
         rec = {
@@ -196,6 +238,46 @@ def main():
 
 
 SEED = 0x5EED2026
+
+
+def bench_standin(args, rank, world):
+    """Launcher test only (tests/test_bench_launcher.py): the contract's rank / barrier /
+    max-over-ranks plumbing on gloo with a CPU stand-in step (a 4 MiB host copy).  It measures
+    nothing about the codec and says so in its line."""
+    import torch.distributed as dist
+    from gobeansdb_amd import shard
+    if world > 1:
+        dist.init_process_group("gloo")
+    a = np.random.default_rng(rank).integers(0, 256, 4 << 20, dtype=np.uint8)
+    b = np.empty_like(a)
+    for _ in range(args.warmup):
+        b[:] = a
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b[:] = a
+    if world > 1:
+        dist.barrier()
+    wall = shard.max_over_ranks([time.perf_counter() - t0])[0]
+    tot = shard.sum_over_ranks({"bytes": a.nbytes * args.steps})
+    if rank == 0:
+        print(json.dumps({"metric": "launcher stand-in (not a measurement)", "value": round(tot["bytes"] / wall / 2**30, 3),
+                          "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(wall * 1e3 / max(args.steps, 1), 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+                          "data": "cpu stand-in: 4 MiB host copy per rank per step",
+                          "config": {"workload": "launcher test", "parallelism": f"shard{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_c5(args):
+    """Config c5 (BASELINE configs[4]): tools/bench_c5.py under the same ranks."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_c5
+    sys.argv = [sys.argv[0], "--warmup", str(max(args.warmup, 1))]
+    return bench_c5.main()
 
 
 def bench_compress(args, rank, world, dev, kind):
@@ -280,7 +362,12 @@ def bench_compress(args, rank, world, dev, kind):
         traffic = round(json.load(open(tj))["hbm_bytes_per_block"] * n)
     cpu = None
     if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline(kind, bs, args.cpu_seconds, mode="compress")
+        ns = min(256, n)
+        dh = dst.data[: int(dst.off[ns - 1]) + bs + 400].cpu().numpy()
+        doff = dst.off[:ns].cpu().numpy()
+        csh = cs[:ns].cpu().numpy()
+        gpu_comp = [dh[int(doff[j]): int(doff[j]) + int(csh[j])].tobytes() for j in range(ns)]
+        cpu = cpu_baseline(kind, bs, args.cpu_seconds, mode="compress", gpu_comp=gpu_comp)
     if rank == 0:
         rec = {
             "metric": "GiB/s device-resident QuickLZ decompress (+compress), batched 4-64 KiB values",
@@ -302,70 +389,107 @@ def bench_compress(args, rank, world, dev, kind):
         torch.distributed.destroy_process_group()
 
 
-REF_WHAT = ("reference quicklz/quicklz.c {fn} (oracle/_ref/libqlzref.so, gcc -O2 as cgo builds it), "
-            "per-thread scratch")
+REF_WHAT = ("reference quicklz/quicklz.c {fn} (oracle/_ref/libqlzref.so, gcc -O2 as cgo builds it)")
 
 
-def cpu_baseline(kind: str, bs: int, seconds: float, mode: str = "decompress"):
-    """Oracle decoder on the host cores over a bounded sample of the same workload."""
+def host_cpus() -> tuple[int, int, str]:
+    """(usable threads, nproc, CPU model).  Usable = the CPUs in this process's affinity mask,
+    capped by the cgroup CPU quota (cpu.max) when one is set: on the GPU box the affinity
+    mask shows the whole machine while the quota grants one GPU's share."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            usable = max(1, min(usable, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, os.cpu_count() or usable, model
+
+
+def cpu_baseline(kind: str, bs: int, seconds: float, mode: str = "decompress", gpu_comp=None):
+    """The reference codec (oracle/_ref) -- else the C restatement -- on the host cores over a
+    bounded sample of the same workload: every usable core (the process's affinity mask;
+    nproc reported beside it), one core, and the cgo-faithful form that allocates the
+    output and scratch per call as quicklz/cquicklz.go:24-49 does.
+
+    gpu_comp: the GPU encoder's bytes for blocks 0.. of the same generator; each must equal
+    the CPU codec's output for that block (sampled bit-exactness of the
+    compressed bytes), else the bench fails."""
     from oracle import oracle as O
-    threads = min(os.cpu_count() or 1, 16)
+    threads, nproc, model = host_cpus()
     L = O.lib()
     Q = O.ref_if_built()  # the reference quicklz.c (oracle/_ref) when built; else the C restatement
     kind_ = "reference" if Q is not None else "port"
-    nblk = 2048 if mode == "decompress" else 256
-    if mode == "compress":
-        plain = [O.gen_text(SEED, i, bs) if kind == "text" else O.gen_image(SEED, i, bs) for i in range(nblk)]
-        off_s, tot_s = _pack(plain)
-        off_d, tot_d = _pack([b"\0" * (bs + 400)] * nblk)
-        srcb = np.zeros(tot_s, np.uint8)
-        for o, p_ in zip(off_s, plain):
-            srcb[int(o): int(o) + len(p_)] = np.frombuffer(p_, np.uint8)
-        lens = np.asarray([len(p_) for p_ in plain], np.uint32)
-        dst = np.zeros(tot_d, np.uint8)
-        reps, ns = 0, 0.0
-        t_end = time.time() + seconds
-        while time.time() < t_end or reps == 0:
-            if Q is not None:
-                ns += L.orc_bench_ref(ctypes.cast(Q.qlz_compress, ctypes.c_void_p).value, srcb.ctypes.data,
-                                      off_s.ctypes.data, lens.ctypes.data, dst.ctypes.data, off_d.ctypes.data,
-                                      nblk, threads, 1)
-            else:
-                ns += L.orc_bench_compress(srcb.ctypes.data, off_s.ctypes.data, lens.ctypes.data,
-                                           dst.ctypes.data, off_d.ctypes.data, nblk, threads, 0)
-            reps += 1
-        gibs = reps * nblk * bs / (ns * 1e-9) / 2**30
-        what = REF_WHAT.format(fn="qlz_compress") if Q is not None else "oracle/qlz_oracle.c orc_compress"
-        return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": kind_,
-                "sample": f"{reps} passes over {nblk} x {bs} B {kind} blocks, {what} (no CRC), "
-                          f"{threads} threads, -O2"}
-    plain = [O.gen_text(0x5EED2026, i, bs) if kind == "text" else O.gen_image(0x5EED2026, i, bs)
-             for i in range(nblk)]
-    comp = [O.compress(p) for p in plain]
-    off_c, tot_c = _pack(comp)
-    off_d, tot_d = _pack(plain)
-    srcb = np.zeros(tot_c, np.uint8)
-    for o, c in zip(off_c, comp):
+    comp_mode = mode == "compress"
+    nblk = max(2048 if not comp_mode else 256, threads * (32 if not comp_mode else 4))
+    nblk = min(nblk, 8192 if not comp_mode else 2048)
+    gen = O.gen_text if kind == "text" else O.gen_image
+    plain = [gen(SEED, i, bs) for i in range(nblk)]
+    if comp_mode:
+        src_list, out_len = plain, bs + 400
+    else:
+        src_list, out_len = [O.compress(p_) for p_ in plain], bs
+    off_s, tot_s = _pack(src_list)
+    off_d, tot_d = _pack([b"\0" * out_len] * nblk)
+    srcb = np.zeros(tot_s, np.uint8)
+    for o, c in zip(off_s, src_list):
         srcb[int(o): int(o) + len(c)] = np.frombuffer(c, np.uint8)
-    lens = np.asarray([len(c) for c in comp], np.uint32)
+    lens = np.asarray([len(c) for c in src_list], np.uint32)
     dst = np.zeros(tot_d, np.uint8)
-    reps, ns = 0, 0.0
-    t_end = time.time() + seconds
-    while time.time() < t_end or reps == 0:
-        if Q is not None:
-            ns += L.orc_bench_ref(ctypes.cast(Q.qlz_decompress, ctypes.c_void_p).value, srcb.ctypes.data,
-                                  off_c.ctypes.data, lens.ctypes.data, dst.ctypes.data, off_d.ctypes.data,
-                                  nblk, threads, 0)
-        else:
-            ns += L.orc_bench_decompress(srcb.ctypes.data, off_c.ctypes.data, lens.ctypes.data,
-                                         dst.ctypes.data, off_d.ctypes.data, nblk, threads, 0)
-        reps += 1
-    if Q is not None and not all(dst[int(o): int(o) + bs].tobytes() == p_ for o, p_ in zip(off_d[:8], plain[:8])):
+    fn = ctypes.cast(Q.qlz_compress if comp_mode else Q.qlz_decompress, ctypes.c_void_p).value if Q else None
+
+    def run(nthr, secs, cgo):
+        reps, ns = 0, 0.0
+        t_end = time.time() + secs
+        while time.time() < t_end or reps == 0:
+            m = (1 if comp_mode else 0) | (2 if cgo else 0)
+            if Q is not None:
+                ns += L.orc_bench_ref(fn, srcb.ctypes.data, off_s.ctypes.data, lens.ctypes.data,
+                                      dst.ctypes.data, off_d.ctypes.data, nblk, nthr, m)
+            elif comp_mode:
+                ns += L.orc_bench_compress(srcb.ctypes.data, off_s.ctypes.data, lens.ctypes.data,
+                                           dst.ctypes.data, off_d.ctypes.data, nblk, nthr, int(cgo))
+            else:
+                ns += L.orc_bench_decompress(srcb.ctypes.data, off_s.ctypes.data, lens.ctypes.data,
+                                             dst.ctypes.data, off_d.ctypes.data, nblk, nthr, int(cgo))
+            reps += 1
+        return reps * nblk * bs / (ns * 1e-9) / 2**30, reps
+
+    parity = None
+    if gpu_comp:
+        for j, g in enumerate(gpu_comp):
+            want = O.compress(plain[j]) if j < len(plain) else O.compress(gen(SEED, j, bs))
+            if g != want:
+                raise SystemExit(f"GPU-compressed block {j} differs from the CPU codec's bytes")
+        parity = f"{len(gpu_comp)} GPU-compressed blocks == oracle/qlz_oracle.c bytes (pinned to quicklz.c)"
+    gibs, reps = run(threads, seconds, False)
+    if not comp_mode and Q is not None and not all(
+            dst[int(o): int(o) + bs].tobytes() == p_ for o, p_ in zip(off_d[:8], plain[:8])):
         raise RuntimeError("reference decompress baseline produced wrong bytes")
-    gibs = reps * nblk * bs / (ns * 1e-9) / 2**30
-    what = REF_WHAT.format(fn="qlz_decompress") if Q is not None else "oracle/qlz_oracle.c orc_decompress"
+    one, _ = run(1, max(2.0, seconds / 5), False)
+    cgo, _ = run(threads, max(2.0, seconds / 3), True)
+    fn_name = "qlz_compress" if comp_mode else "qlz_decompress"
+    what = REF_WHAT.format(fn=fn_name) if Q is not None else f"oracle/qlz_oracle.c orc_{mode}"
+    unit_what = "input" if comp_mode else "output"
     return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": kind_,
-            "sample": f"{reps} passes over {nblk} x {bs} B {kind} blocks, {what}, {threads} threads, -O2"}
+            "sample": f"{reps} passes over {nblk} x {bs} B {kind} blocks, {what}, {threads} threads "
+                      f"(one scratch per thread), GiB/s of {unit_what}" + ("" if comp_mode else "; no CRC"),
+            "threads": threads, "nproc": nproc, "cpu_model": model,
+            "one_core": round(one, 3),
+            "cgo_faithful": round(cgo, 3),
+            "cgo_faithful_what": "per call: output + scratch malloc/free as quicklz/cquicklz.go:24-49",
+            "compress_parity": parity}
 
 
 def _pack(blocks):

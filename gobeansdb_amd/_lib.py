@@ -17,9 +17,9 @@ LIB_PATH = os.environ.get("QLZX_LIB", os.path.join(HERE, "libqlzx.so"))
 HEADER = os.path.join(ROOT, "include", "qlzx.h")
 
 # enum qlzx_status
-OK, E_SIZE_COMPRESSED, E_CORRUPT, E_LEVEL, E_DST_CAP, E_CRC, E_HEADER, E_EMPTY, E_TOO_LARGE = range(9)
+OK, E_SIZE_COMPRESSED, E_CORRUPT, E_LEVEL, E_DST_CAP, E_CRC, E_HEADER, E_EMPTY, E_TOO_LARGE, E_MAX_DSIZE = range(10)
 STATUS_NAMES = ["OK", "E_SIZE_COMPRESSED", "E_CORRUPT", "E_LEVEL", "E_DST_CAP", "E_CRC",
-                "E_HEADER", "E_EMPTY", "E_TOO_LARGE"]
+                "E_HEADER", "E_EMPTY", "E_TOO_LARGE", "E_MAX_DSIZE"]
 
 
 F_GO_COMPAT = 1

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -242,48 +243,69 @@ int qlzx_vhash_batch(const uint8_t *src, const uint64_t *off, const uint32_t *le
 }  // extern "C"
 
 /* ---------------- single-call runtime (quicklz.h drop-in on the GPU) ----------------
- * Each calling thread owns a stream and device/pinned staging buffers, so the
- * symbols are re-entrant like the reference (quicklz.h: one scratch per call). */
+ * Each calling thread owns a stream, a device buffer and a pinned host buffer, so the
+ * symbols are re-entrant like the reference (quicklz.h: one scratch per call).  A call
+ * copies the caller's bytes into the pinned buffer, does one H2D, the kernel, one D2H of
+ * the result and its descriptor, and one stream synchronisation; the caller's pageable
+ * buffers are touched only by host memcpy. */
 namespace {
 
-struct Ctx {
-    hipStream_t s = nullptr;
-    uint8_t *d_buf = nullptr;  // [src | dst | meta | ws]
-    size_t d_cap = 0;
-    uint8_t *h_meta = nullptr;  // pinned 4 KiB
-    bool ok = false;
-    ~Ctx() {
-        if (d_buf) (void)hipFree(d_buf);
-        if (h_meta) (void)hipHostFree(h_meta);
-        if (s) (void)hipStreamDestroy(s);
-    }
-    int init() {
-        if (ok) return 0;
-        int ndev = 0;
-        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(QLZX_R_NO_DEVICE, "no HIP device");
-        HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        HIP_OK(hipHostMalloc((void **)&h_meta, 4096, hipHostMallocDefault));
-        ok = true;
-        return 0;
-    }
-    int reserve(size_t bytes) {
-        if (bytes <= d_cap) return 0;
-        if (d_buf) (void)hipFree(d_buf);
-        d_buf = nullptr;
-        d_cap = 0;
-        const size_t want = align_up(bytes + bytes / 4, 1 << 20);
-        HIP_OK(hipMalloc((void **)&d_buf, want));
-        d_cap = want;
-        return 0;
-    }
-};
-thread_local Ctx t_ctx;
+// Set by an atexit handler registered at the first context init, i.e. after the HIP runtime
+// registered its own teardown (atexit runs in reverse order): contexts destroyed after that
+// (threads exiting during process exit) skip the HIP frees.
+std::atomic<bool> g_hip_down{false};
+void mark_hip_down() { g_hip_down.store(true); }
 
 struct Meta {  // one-block batch descriptors, device side
     uint64_t src_off, dst_off;
     uint32_t src_len, dst_cap, out_size, crc_in, crc_out;
     int32_t status;
 };
+
+struct Ctx {
+    hipStream_t s = nullptr;
+    uint8_t *d_buf = nullptr;  // [meta 256 | src | dst | ws]
+    size_t d_cap = 0;
+    uint8_t *h_buf = nullptr;  // pinned: [meta 256 | staging]
+    size_t h_cap = 0;
+    bool ok = false;
+    ~Ctx() {
+        if (g_hip_down.load()) return;
+        if (d_buf) (void)hipFree(d_buf);
+        if (h_buf) (void)hipHostFree(h_buf);
+        if (s) (void)hipStreamDestroy(s);
+    }
+    int init() {
+        if (ok) return 0;
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(QLZX_R_NO_DEVICE, "no HIP device");
+        static std::once_flag once;
+        std::call_once(once, [] { std::atexit(mark_hip_down); });
+        HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        ok = true;
+        return 0;
+    }
+    int reserve(size_t dev_bytes, size_t host_bytes) {
+        if (dev_bytes > d_cap) {
+            if (d_buf) (void)hipFree(d_buf);
+            d_buf = nullptr;
+            d_cap = 0;
+            const size_t want = align_up(dev_bytes + dev_bytes / 4, 1 << 20);
+            HIP_OK(hipMalloc((void **)&d_buf, want));
+            d_cap = want;
+        }
+        if (host_bytes > h_cap) {
+            if (h_buf) (void)hipHostFree(h_buf);
+            h_buf = nullptr;
+            h_cap = 0;
+            const size_t want = align_up(host_bytes + host_bytes / 4, 1 << 20);
+            HIP_OK(hipHostMalloc((void **)&h_buf, want, hipHostMallocDefault));
+            h_cap = want;
+        }
+        return 0;
+    }
+};
+thread_local Ctx t_ctx;
 
 }  // namespace
 
@@ -300,23 +322,27 @@ size_t qlzx_compress1(const void *source, char *destination, size_t size, uint32
     if (c.init()) return 0;
     const size_t src_b = align_up(size, 256), dst_b = align_up(size + 400, 256);
     const size_t ws_b = qlzx_compress_workspace_size(1, (uint32_t)size);
-    if (c.reserve(src_b + dst_b + 256 + ws_b)) return 0;
-    uint8_t *d_src = c.d_buf, *d_dst = d_src + src_b, *d_meta = d_dst + dst_b, *d_ws = d_meta + 256;
-    Meta *m = (Meta *)c.h_meta;
+    // pinned: [meta | src staging, reused for the result]
+    if (c.reserve(256 + src_b + dst_b + ws_b, 256 + std::max(src_b, dst_b))) return 0;
+    uint8_t *d_meta = c.d_buf, *d_src = d_meta + 256, *d_dst = d_src + src_b, *d_ws = d_dst + dst_b;
+    Meta *m = (Meta *)c.h_buf;
+    uint8_t *h_data = c.h_buf + 256;
     memset(m, 0, sizeof(Meta));
     m->src_len = (uint32_t)size;
-    if (hipMemcpyAsync(d_src, source, size, hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
-    if (hipMemcpyAsync(d_meta, m, sizeof(Meta), hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
+    memcpy(h_data, source, size);
+    // one H2D of descriptor + source (contiguous on both sides)
+    if (hipMemcpyAsync(d_meta, c.h_buf, 256 + size, hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
     Meta *dm = (Meta *)d_meta;
     qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
     if (qlzx_compress_batch(&b, &dm->out_size, &dm->status, nullptr, nullptr, (uint32_t)size, flags, d_ws,
                             ws_b, c.s))
         return 0;
-    if (hipMemcpyAsync(m, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
+    // one D2H of descriptor + the largest possible result, then the only synchronisation
+    if (hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
+    if (hipMemcpyAsync(h_data, d_dst, size + 400, hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
     if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
-    if (m->status != QLZX_OK || m->out_size == 0) return 0;
-    if (hipMemcpyAsync(destination, d_dst, m->out_size, hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
-    if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
+    if (m->status != QLZX_OK || m->out_size == 0 || m->out_size > size + 400) return 0;
+    memcpy(destination, h_data, m->out_size);
     return m->out_size;
 }
 
@@ -328,24 +354,25 @@ size_t qlz_decompress(const char *source, void *destination, char *scratch_decom
     if (c.init()) return 0;
     const size_t src_b = align_up(csize, 256), dst_b = align_up(dsize + 1, 256);
     const size_t ws_b = align_up(qlzx_decompress_workspace_size(1, (uint32_t)dsize), 256);
-    if (c.reserve(src_b + dst_b + 256 + ws_b)) return 0;
-    uint8_t *d_src = c.d_buf, *d_dst = d_src + src_b, *d_meta = d_dst + dst_b, *d_ws = d_meta + 256;
-    Meta *m = (Meta *)c.h_meta;
+    if (c.reserve(256 + src_b + dst_b + ws_b, 256 + std::max(src_b, dst_b))) return 0;
+    uint8_t *d_meta = c.d_buf, *d_src = d_meta + 256, *d_dst = d_src + src_b, *d_ws = d_dst + dst_b;
+    Meta *m = (Meta *)c.h_buf;
+    uint8_t *h_data = c.h_buf + 256;
     memset(m, 0, sizeof(Meta));
     m->src_len = (uint32_t)csize;
     m->dst_cap = (uint32_t)dsize;
-    if (hipMemcpyAsync(d_src, source, csize, hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
-    if (hipMemcpyAsync(d_meta, m, sizeof(Meta), hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
+    memcpy(h_data, source, csize);
+    if (hipMemcpyAsync(d_meta, c.h_buf, 256 + csize, hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
     Meta *dm = (Meta *)d_meta;
     qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
     if (qlzx_decompress_batch(&b, &dm->dst_cap, &dm->out_size, &dm->status, nullptr, nullptr, nullptr,
                               (uint32_t)dsize, d_ws, ws_b, c.s))
         return 0;
-    if (hipMemcpyAsync(m, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
+    if (hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
+    if (dsize && hipMemcpyAsync(h_data, d_dst, dsize, hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
     if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
     if (m->status != QLZX_OK) return 0;
-    if (dsize && hipMemcpyAsync(destination, d_dst, dsize, hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
-    if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
+    memcpy(destination, h_data, dsize);
     return m->out_size;
 }
 
@@ -354,17 +381,17 @@ uint32_t crc32_write(uint32_t crc, unsigned char *buf, int len) {
     Ctx &c = t_ctx;
     if (c.init()) return crc;
     const size_t src_b = align_up((size_t)len, 256);
-    if (c.reserve(src_b + 256)) return crc;
-    uint8_t *d_src = c.d_buf, *d_meta = d_src + src_b;
-    Meta *m = (Meta *)c.h_meta;
+    if (c.reserve(256 + src_b, 256 + src_b)) return crc;
+    uint8_t *d_meta = c.d_buf, *d_src = d_meta + 256;
+    Meta *m = (Meta *)c.h_buf;
     memset(m, 0, sizeof(Meta));
     m->src_len = (uint32_t)len;
     m->crc_in = crc;
-    if (hipMemcpyAsync(d_src, buf, len, hipMemcpyHostToDevice, c.s) != hipSuccess) return crc;
-    if (hipMemcpyAsync(d_meta, m, sizeof(Meta), hipMemcpyHostToDevice, c.s) != hipSuccess) return crc;
+    memcpy(c.h_buf + 256, buf, (size_t)len);
+    if (hipMemcpyAsync(d_meta, c.h_buf, 256 + (size_t)len, hipMemcpyHostToDevice, c.s) != hipSuccess) return crc;
     Meta *dm = (Meta *)d_meta;
     if (qlzx_crc32_batch(d_src, &dm->src_off, &dm->src_len, 1, &dm->crc_in, 0, &dm->crc_out, c.s)) return crc;
-    if (hipMemcpyAsync(m, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return crc;
+    if (hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return crc;
     if (hipStreamSynchronize(c.s) != hipSuccess) return crc;
     return m->crc_out;
 }

@@ -35,6 +35,7 @@ constexpr uint32_t kSpRecChunk = 16;             // groups per record DMA (64 la
 constexpr uint32_t kSpRecRing = 2 * kSpRecChunk; // groups resident
 constexpr uint32_t kSpMq = 256;                  // match ring entries (two IP batches + carries)
 constexpr uint32_t kSpCov = 2048;                // coverage bitmap reach (64 words)
+constexpr uint32_t kMaxDevices = 64;             // per-device side streams of the launcher
 #ifndef QLZX_SP_WIN
 #define QLZX_SP_WIN 4096
 #endif
@@ -522,16 +523,40 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         return !(e && e[0] == '0');
     }();
     const bool overlap = overlap_env && ws_bytes >= 2 * one && b.n > chunk;
-    // per host thread (the batch API is re-entrant like the reference); the side stream
-    // belongs to the device that was current at the thread's first overlapped call
-    thread_local hipStream_t side = nullptr;
-    thread_local hipEvent_t ev_k1[2], ev_k2[2];
-    if (overlap && !side) {
-        if (hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess) return (int)hipErrorUnknown;
-        for (int j = 0; j < 2; j++) {
-            (void)hipEventCreateWithFlags(&ev_k1[j], hipEventDisableTiming);
-            (void)hipEventCreateWithFlags(&ev_k2[j], hipEventDisableTiming);
+    // per host thread (the batch API is re-entrant like the reference) and per device: the
+    // side stream and events are created on the device that owns `s`
+    struct Side {
+        hipStream_t st = nullptr;
+        hipEvent_t k1[2], k2[2];
+    };
+    thread_local Side sides[kMaxDevices];
+    hipStream_t side = nullptr;
+    hipEvent_t *ev_k1 = nullptr, *ev_k2 = nullptr;
+    if (overlap) {
+        int dev = 0, cur = 0;
+        if (s) {
+            hipDevice_t hd;
+            if (hipStreamGetDevice(s, &hd) != hipSuccess) return (int)hipErrorInvalidResourceHandle;
+            dev = (int)hd;
+        } else if (hipGetDevice(&dev) != hipSuccess) {
+            return (int)hipErrorNoDevice;
         }
+        if (dev < 0 || dev >= (int)kMaxDevices) return (int)hipErrorInvalidDevice;
+        Side &sd = sides[dev];
+        if (!sd.st) {
+            (void)hipGetDevice(&cur);
+            if (cur != dev) (void)hipSetDevice(dev);
+            hipError_t e = hipStreamCreateWithFlags(&sd.st, hipStreamNonBlocking);
+            for (int j = 0; j < 2 && e == hipSuccess; j++) {
+                e = hipEventCreateWithFlags(&sd.k1[j], hipEventDisableTiming);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&sd.k2[j], hipEventDisableTiming);
+            }
+            if (cur != dev) (void)hipSetDevice(cur);
+            if (e != hipSuccess) return (int)e;
+        }
+        side = sd.st;
+        ev_k1 = sd.k1;
+        ev_k2 = sd.k2;
     }
     // QLZX_K2=split: the item-phase/match-phase kernel (k_dec_split, DESIGN.md §4 "Round 2:
     // the split K2"); default: the item-per-lane kernel k_dec_blocks, which measured faster
@@ -561,11 +586,13 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         if (crc)
             hipLaunchKernelGGL(k_dec_parse<true>, dim3((cnt + kParseWG<true> - 1) / kParseWG<true>),
                                dim3(kParseWG<true>), 0, s1, b,
-                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order);
+                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order,
+                               max_dsize);
         else
             hipLaunchKernelGGL(k_dec_parse<false>, dim3((cnt + kParseWG<false> - 1) / kParseWG<false>),
                                dim3(kParseWG<false>), 0, s1, b,
-                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order);
+                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order,
+                               max_dsize);
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
 #ifndef QLZX_EXP_K2_EXTRA_LDS
 #define QLZX_EXP_K2_EXTRA_LDS 0  // experiments: extra dynamic LDS per WG to lower occupancy

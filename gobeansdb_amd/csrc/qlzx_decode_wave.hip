@@ -16,16 +16,18 @@
 //     base is wave-uniform and no register waits on in-flight loads.  A lane
 //     parses until it runs out of landed bytes, so rounds self-align by bytes.
 //
-// K2 k_dec_blocks one WAVE per block, the whole output block resident in LDS.
-//     Items are decoded 64 at a time, one per lane.  Item k of group g sits at
+// K2 k_dec_blocks one WAVE per block; output goes through a sliding LDS window of
+//     kWin bytes (older output is flushed to HBM and read back from there by
+//     "far" matches).  Items are decoded 64 at a time, one per lane.  Item k of
+//     group g sits at
 //       ip + 4 + k + popc(a & low(k)) + 2 popc(b & low(k)),
-//     so no serial walk is needed.  Group records (two batches ahead) and
-//     token bytes (one batch ahead) are DMA'd into LDS while the current batch
-//     resolves.  Per batch: decode tokens, DPP-scan output lengths, validate
-//     (checks C1-C5), write literals, then copy matches in
-//     sub-rounds: a match is copied once every source byte it needs lies below
-//     the first pending match (the lowest pending match is always ready, so
-//     every sub-round makes progress).  The finished block leaves LDS in
+//     so no serial walk is needed.  Group records (kRecAhead batches ahead) and
+//     token dwords (kTokAhead batches ahead) are DMA'd into LDS while the
+//     current batch resolves.  Per batch: decode tokens, DPP-scan output lengths,
+//     validate (checks C1-C5), write literals, then copy matches in
+//     sub-rounds: a match is copied once none of the lanes producing its source
+//     bytes is pending (the lowest pending match is always ready, so every
+//     sub-round makes progress).  The finished block leaves LDS in
 //     16-B-per-lane coalesced stores.
 #include "qlzx_device.h"
 
@@ -73,8 +75,10 @@ constexpr uint32_t kTokSlots = kTokAhead;      // batches bt .. bt+kTokAhead-1 (
 constexpr uint32_t kRecSlots = kTokAhead + 1;  // batches bt+kTokAhead .. bt+kRecAhead
 constexpr uint32_t kSubMax = 64 * 32;          // K2 sub-batch output bound: the 64-word item-start bitmap
 #ifndef QLZX_K2_VMWAIT
-#define QLZX_K2_VMWAIT 6  // = 2 * QLZX_K2_SLACK (set both together); other values break the prefetch invariant
+#define QLZX_K2_VMWAIT (2 * QLZX_K2_SLACK)  // two DMA instructions per iteration
 #endif
+static_assert(QLZX_K2_VMWAIT == 2 * QLZX_K2_SLACK,
+              "K2 waits for the DMAs of iterations <= bt - slack: two per iteration");
 
 __host__ __device__ inline uint32_t groups_max(uint32_t max_dsize) { return max_dsize / 31u + 2u; }
 
@@ -192,7 +196,7 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
                                                          const uint32_t *crc_state, const uint32_t *crc_expect,
                                                          uint32_t *crc_out, uint32_t first, uint32_t count,
                                                          BlkInfo *info, GroupRec *recs, uint32_t gmax,
-                                                         const uint32_t *order) {
+                                                         const uint32_t *order, uint32_t max_dsize) {
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG<CRC> / 64) * kRingWave];
     __shared__ uint32_t tab[CRC ? 8 * 256 : 1];
     if (CRC) {
@@ -222,6 +226,7 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
                 if (h.csize != len) st = QLZX_E_SIZE_COMPRESSED;
                 else if (h.level != 3) st = QLZX_E_LEVEL;
                 else if (dst_cap && h.dsize > dst_cap[i]) st = QLZX_E_DST_CAP;
+                else if (h.dsize > max_dsize) st = QLZX_E_MAX_DSIZE;     // the caller's bound is wrong
                 else if (h.dsize > QLZX_FAST_MAX_DSIZE) st = kPending;  // general path owns it
                 else if (!h.compressed) {
                     if (csize >= hdr + dsize) kind = kBlkStored;
@@ -378,8 +383,8 @@ template <uint32_t W>
 struct K2Lds {
     uint8_t pad[16];                 // a source dword may start 4 B before win[0]
     uint8_t win[W + 32];             // reads run <= 24 B past a write; win[W + 24] = literal dummy
-    GroupRec rec[kRecSlots][4];      // records of the <= 4 groups of batches bt+4..bt+8
-    uint32_t tok[kTokSlots][64];     // per-lane token dword of batches bt..bt+3
+    GroupRec rec[kRecSlots][4];      // records of the <= 4 groups of batches bt+kTokAhead .. bt+kRecAhead
+    uint32_t tok[kTokSlots][64];     // per-lane token dword of batches bt .. bt+kTokAhead-1
 };  // the window first: copy addresses fit the DS instructions' immediate offsets
 
 // Every K2 iteration issues exactly 2 DMA instructions (1 token dword + 1
@@ -587,10 +592,11 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
     uint32_t base = 0;                // window start (multiple of W/2)
     bool err = false;                 // per-lane: a check failed on this lane's item
     bool tail = false, complete = dsize == 0;
-    // slot counters: tokens of bt (read) and bt+4 (issue); records of bt+4 (read) and bt+8 (issue)
+    // slot counters: tokens of bt (read) and bt+kTokAhead (issue); records of bt+kTokAhead (read)
+    // and bt+kRecAhead (issue)
     uint32_t ts = 0, rs4 = kTokAhead % kRecSlots, rs8 = kRecAhead % kRecSlots;
     for (uint32_t bt = 0; bt < nb && !complete; bt++) {
-        // this batch's token dword, and the record the prefetch of batch bt+4 needs;
+        // this batch's token dword, and the record the prefetch of batch bt+kTokAhead needs;
         // both reads complete before that prefetch reuses this batch's token slot
         const uint32_t tw = L.tok[ts][lane];
         const bool v4 = (bt + kTokAhead) * 64 + lane < nitems;
@@ -599,7 +605,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
         const uint32_t posm = pm[0];
 #pragma unroll
         for (uint32_t j = 0; j + 1 < kTokAhead; j++) pm[j] = pm[j + 1];
-        // the token DMA of batch bt+4 goes out at the end of the iteration: until then
+        // the token DMA of batch bt+kTokAhead goes out at the end of the iteration: until then
         // this batch's token slot holds the item-start bitmap of the sub-batches
         uint32_t tokp;
         pm[kTokAhead - 1] = issue_tok<false>(gr4, cur, v4, nullptr, src, csize, &tokp);
@@ -749,8 +755,9 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             if (__ballot(err)) { more = false; complete = false; }
         }
         if (__ballot(err)) break;
-        dma4(src + tokp, lds_addr(bm));  // tokens of batch bt+4 into the slot bt used (bitmap done)
-        asm volatile("s_waitcnt vmcnt(" QLZX_STR(QLZX_K2_VMWAIT) ")" ::: "memory");  // DMAs of iterations <= bt-3 landed
+        dma4(src + tokp, lds_addr(bm));  // tokens of batch bt+kTokAhead into the slot bt used (bitmap done)
+        // DMAs of iterations <= bt - kK2Slack have landed
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QLZX_K2_VMWAIT) : "memory");
         PROF_MARK(4);  // 4: waiting for prefetch
     }
     vm_sync();

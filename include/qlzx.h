@@ -61,7 +61,8 @@ enum qlzx_status {
     QLZX_E_CRC = 5,             /* record CRC mismatch (store/datafile.go:161-168) */
     QLZX_E_HEADER = 6,          /* src_len shorter than the header */
     QLZX_E_EMPTY = 7,           /* compress of an empty value (cquicklz.go:36 panics) */
-    QLZX_E_TOO_LARGE = 8        /* compress size > 0xffffffff-400 (quicklz.c:705) */
+    QLZX_E_TOO_LARGE = 8,       /* compress size > 0xffffffff-400 (quicklz.c:705) */
+    QLZX_E_MAX_DSIZE = 9        /* dsize > the batch's max_dsize argument (caller contract) */
 };
 
 enum qlzx_return {
@@ -94,7 +95,8 @@ typedef struct qlzx_blocks {
  *   crc_expect[i] in: stored record CRC (header[0:4]); nullable = no check
  *   crc_out[i]   out: ~crc_write(crc_state, compressed value)    (nullable)
  *   max_dsize    upper bound on dsize over the batch (selects kernels; blocks
- *                above the fast-path limit take the general kernel)
+ *                above the fast-path limit take the general kernel).  A block whose
+ *                header dsize exceeds it is not decoded: status QLZX_E_MAX_DSIZE.
  * The record CRC is computed over the compressed bytes in the same pass that
  * decodes them (fused). */
 size_t qlzx_decompress_workspace_size(uint32_t n, uint32_t max_dsize);

@@ -28,11 +28,13 @@ def append(rec) -> bytes:
     return out + bytes((-len(out)) % PADDING)
 
 
-def gc_rewrite(data: bytes, keep, data_file_max: int, dst_head: int = 0):
+def gc_rewrite(data: bytes, keep, data_file_max: int, dst_head: int = 0, next_heads=()):
     """Kept records of `data` (keep[i] for the i-th record the reader returns), rewritten in
     order: returns (chunks, positions) with chunks[j] = the bytes written into the j-th
-    destination chunk (the first starting at dst_head, later ones fresh) and positions[i] =
-    (chunk index, offset) of each kept record."""
+    destination chunk and positions[i] = (chunk index, offset) of each kept record.  The first
+    destination chunk starts at dst_head, destination chunk j >= 1 at next_heads[j - 1]
+    (0 past the list): beginGCWriting appends at the chunk's size unless it rewrites the
+    source chunk itself (store/datachunk.go:185-193)."""
     recs, _ = stream_all(data)
     chunks = [bytearray()]
     head = dst_head
@@ -43,7 +45,8 @@ def gc_rewrite(data: bytes, keep, data_file_max: int, dst_head: int = 0):
         recsize = (HDR + len(r.key) + len(r.body) + 255) >> 8 << 8
         if recsize + head > data_file_max:                # gc.go:320: next destination chunk
             chunks.append(bytearray())
-            head = 0
+            j = len(chunks) - 1
+            head = next_heads[j - 1] if j - 1 < len(next_heads) else 0
         b = append(r)
         pos.append((len(chunks) - 1, head))
         chunks[-1] += b

@@ -155,7 +155,15 @@ def ref_if_built():
     L = lib()
     L.orc_bench_ref.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
     L.orc_bench_ref.restype = ctypes.c_double
+    L.orc_bench_replay.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    L.orc_bench_replay.restype = ctypes.c_double
     return Q
+
+
+def crc_ref_if_built():
+    """The compiled reference crc32_write (oracle/_ref/libcrc32ref.so) if present."""
+    c = os.path.join(HERE, "_ref", "libcrc32ref.so")
+    return ctypes.CDLL(c) if os.path.exists(c) else None
 
 
 def ref_compress(data: bytes) -> bytes:

@@ -380,15 +380,33 @@ typedef struct {
     uint32_t lo, hi; void *fn; int mode;
 } rjob_t;
 
+/* mode bit 0: 0 decompress, 1 compress.  Bit 1 (cgo-faithful): every call allocates what
+ * the Go wrappers allocate -- CCompress a len+400 output CArray and a 528,400-B scratch
+ * (quicklz/cquicklz.go:24-34), CDecompress a dsize output CArray and a 16-B buffer
+ * (cquicklz.go:45-49) -- and frees them after copying one byte out (so the call cannot be
+ * elided); otherwise each thread owns one scratch and writes into dst. */
 static void *run_rjob(void *arg) {
     rjob_t *j = (rjob_t *)arg;
-    char *scratch = (char *)malloc(j->mode ? 528400 : 16);
-    if (j->mode) memset(scratch, 0, 528400);
+    const int comp = j->mode & 1, cgo = (j->mode >> 1) & 1;
+    char *scratch = cgo ? NULL : (char *)malloc(comp ? 528400 : 16);
+    if (scratch && comp) memset(scratch, 0, 528400);
     for (uint32_t i = j->lo; i < j->hi; i++) {
         const uint8_t *s = j->src + j->src_off[i];
         uint8_t *d = j->dst + j->dst_off[i];
-        if (j->mode == 0) ((ref_dec_fn)j->fn)((const char *)s, d, scratch);
-        else ((ref_comp_fn)j->fn)(s, (char *)d, j->src_len[i], scratch);
+        if (cgo) {
+            const size_t outn = comp ? (size_t)j->src_len[i] + 400 : orc_size_decompressed(s);
+            uint8_t *out = (uint8_t *)malloc(outn ? outn : 1);
+            char *sc = (char *)malloc(comp ? 528400 : 16);
+            if (comp) ((ref_comp_fn)j->fn)(s, (char *)out, j->src_len[i], sc);
+            else ((ref_dec_fn)j->fn)((const char *)s, out, sc);
+            d[0] = out[0];
+            free(sc);
+            free(out);
+        } else if (!comp) {
+            ((ref_dec_fn)j->fn)((const char *)s, d, scratch);
+        } else {
+            ((ref_comp_fn)j->fn)(s, (char *)d, j->src_len[i], scratch);
+        }
     }
     free(scratch);
     return NULL;
@@ -409,6 +427,96 @@ double orc_bench_ref(void *fn, const uint8_t *src, const uint64_t *src_off, cons
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
     clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(th);
+    free(jobs);
+    return (t1.tv_sec - t0.tv_sec) * 1e9 + (t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ---- c4 CPU baseline: the reference record loop (test infrastructure / baseline only) ----
+ * One thread per range of records, each walking its range the way
+ * store/bucket.go:89-117 (buildHintFromData) drives DataStreamReader.Next
+ * (store/datafile.go:228-277): decode the 24-B header, CRC-verify
+ * header[4:24] | key | value with the reference crc32_write (store/datafile.go:66-76,
+ * 161-168), Payload.Decompress through the reference qlz_decompress when FLAG_COMPRESS
+ * is set (store/item.go:163-176; cgo = 1 allocates the output as CDecompress does),
+ * then Getvhash (store/item.go:89-100, utils/hash.go:8-16).  Returns the wall time in ns;
+ * *bad counts records whose CRC or decompress failed (0 on a valid chunk). */
+typedef uint32_t (*ref_crc_fn)(uint32_t, unsigned char *, int);
+typedef struct {
+    const uint8_t *data; uint64_t lo, hi; void *dec; void *crc; int cgo;
+    uint64_t bad; uint32_t hsum;
+} pjob_t;
+
+static uint32_t fnv1a_sx(const uint8_t *p, size_t n) {  /* utils/hash.go:8-16 */
+    uint32_t h = 0x811C9DC5u;
+    for (size_t i = 0; i < n; i++) {
+        h ^= (uint32_t)(int32_t)(int8_t)p[i];
+        h *= 0x01000193u;
+    }
+    return h;
+}
+static uint16_t getvhash(const uint8_t *v, size_t n) {  /* store/item.go:89-100 */
+    uint32_t h = (uint32_t)n * 97u;
+    if (n <= 1024) h += fnv1a_sx(v, n);
+    else {
+        h += fnv1a_sx(v, 512);
+        h *= 97u;
+        h += fnv1a_sx(v + n - 512, 512);
+    }
+    return (uint16_t)h;
+}
+
+static void *run_pjob(void *arg) {
+    pjob_t *j = (pjob_t *)arg;
+    ref_crc_fn crc = (ref_crc_fn)j->crc;
+    ref_dec_fn dec = (ref_dec_fn)j->dec;
+    char scratch[16];
+    uint8_t *reuse = (uint8_t *)malloc(64u << 20);
+    uint64_t pos = j->lo;
+    while (pos + 24 <= j->hi) {
+        const uint8_t *h = j->data + pos;
+        const uint32_t stored = ld32(h), flag = ld32(h + 8), ksz = ld32(h + 16), vsz = ld32(h + 20);
+        const uint8_t *key = h + 24, *val = key + ksz;
+        uint32_t c = crc(0xFFFFFFFFu, (unsigned char *)h + 4, 20);
+        if (ksz) c = crc(c, (unsigned char *)key, (int)ksz);
+        if (vsz) c = crc(c, (unsigned char *)val, (int)vsz);
+        if (~c != stored) j->bad++;
+        const uint8_t *body = val;
+        size_t blen = vsz;
+        uint8_t *tmp = NULL;
+        if (flag & 0x10000u) {
+            const size_t dsz = orc_size_decompressed(val);
+            uint8_t *out = j->cgo ? (tmp = (uint8_t *)malloc(dsz ? dsz : 1)) : reuse;
+            if (dec((const char *)val, out, scratch) != dsz) j->bad++;
+            body = out;
+            blen = dsz;
+        }
+        j->hsum += getvhash(body, blen);
+        free(tmp);
+        pos += (24 + (uint64_t)ksz + vsz + 255) & ~(uint64_t)255;
+    }
+    free(reuse);
+    return NULL;
+}
+
+double orc_bench_replay(void *dec, void *crc, const uint8_t *data, const uint64_t *cuts, int threads, int cgo,
+                        uint64_t *bad) {
+    if (threads < 1) threads = 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+    pjob_t *jobs = (pjob_t *)malloc(sizeof(pjob_t) * threads);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (pjob_t){data, cuts[t], cuts[t + 1], dec, crc, cgo, 0, 0};
+        pthread_create(&th[t], NULL, run_pjob, &jobs[t]);
+    }
+    uint64_t b = 0;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        b += jobs[t].bad;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (bad) *bad = b;
     free(th);
     free(jobs);
     return (t1.tv_sec - t0.tv_sec) * 1e9 + (t1.tv_nsec - t0.tv_nsec);

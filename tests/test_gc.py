@@ -51,27 +51,29 @@ def test_plan_matches_oracle_rotation(seed):
     recs, _ = R.stream_all(data)
     rnd = random.Random(seed)
     keep = [rnd.random() < 0.6 for _ in recs]
-    for dfm, head in ((1 << 30, 0), (4096, 0), (2560, 1024), (700, 0)):
-        _, pos = G.gc_rewrite(data, keep, data_file_max=dfm, dst_head=head)
+    for dfm, head, nxt in ((1 << 30, 0, ()), (4096, 0, ()), (2560, 1024, ()), (700, 0, ()),
+                           (4096, 1024, (512, 3840, 256)), (2560, 0, (2048,))):
+        _, pos = G.gc_rewrite(data, keep, data_file_max=dfm, dst_head=head, next_heads=nxt)
         rs = np.asarray([r.rsize for r, k in zip(recs, keep) if k], np.int64)
-        chunk, off = gc.plan(rs, head, dfm)
-        assert [(int(c), int(o)) for c, o in zip(chunk, off)] == pos, (dfm, head)
+        chunk, off = gc.plan(rs, head, dfm, nxt)
+        assert [(int(c), int(o)) for c, o in zip(chunk, off)] == pos, (dfm, head, nxt)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,dfm,head", [(5, 1 << 30, 0), (6, 8192, 0), (7, 4096, 2048), (8, 600, 0)])
-def test_gpu_rewrite_matches_oracle(seed, dfm, head):
+@pytest.mark.parametrize("seed,dfm,head,nxt", [(5, 1 << 30, 0, ()), (6, 8192, 0, ()), (7, 4096, 2048, ()),
+                                              (8, 600, 0, ()), (10, 4096, 1024, (512, 3584))])
+def test_gpu_rewrite_matches_oracle(seed, dfm, head, nxt):
     import torch
     from gobeansdb_amd import gc, replay
     data = _chunk(seed, 150)
     recs, _ = R.stream_all(data)
     rnd = random.Random(seed)
     keep = [rnd.random() < 0.55 for _ in recs]
-    want_chunks, want_pos = G.gc_rewrite(data, keep, data_file_max=dfm, dst_head=head)
+    want_chunks, want_pos = G.gc_rewrite(data, keep, data_file_max=dfm, dst_head=head, next_heads=nxt)
     d = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).cuda()
     off, broken, end_err, _, _ = replay.index(d)
     assert off.numel() == len(recs)
-    res = gc.rewrite(d, off, torch.tensor(keep, device="cuda"), dst_head=head, data_file_max=dfm)
+    res = gc.rewrite(d, off, torch.tensor(keep, device="cuda"), dst_head=head, data_file_max=dfm, next_heads=nxt)
     torch.cuda.synchronize()
     assert [c.cpu().numpy().tobytes() for c in res.chunks] == want_chunks
     assert [(int(c), int(o)) for c, o in zip(res.chunk, res.offset)] == want_pos

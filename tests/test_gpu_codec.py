@@ -255,3 +255,24 @@ def test_mixed_sizes_block_order_round_trip(cuda, k2):
     assert int((st2 != 0).sum()) == 0
     assert torch.equal(dsz, plen)
     assert torch.equal(batch.crc32(out), expect)
+
+
+def test_max_dsize_contract(cuda):
+    """A block whose header dsize exceeds the batch's max_dsize argument is reported as
+    QLZX_E_MAX_DSIZE (not left pending, not misreported as corrupt); the others decode."""
+    import torch
+    from gobeansdb_amd import _lib, batch
+    sizes = [4000, 20000, 70000, 16000]
+    plain = [O.gen_text(3, i, n) for i, n in enumerate(sizes)]
+    comp = [O.compress(p) for p in plain]
+    src = batch.BlockBatch.from_bytes(comp)
+    for md in (16384, 65536):
+        out = batch.BlockBatch.empty_for(sizes)
+        dsz, st, _ = batch.decompress(src, out, max_dsize=md)
+        torch.cuda.synchronize()
+        st = st.cpu().numpy().tolist()
+        assert st == [0 if n <= md else _lib.E_MAX_DSIZE for n in sizes], (md, st)
+        got = out.to_bytes(dsz.cpu().numpy())
+        for n, p, g, s in zip(sizes, plain, got, st):
+            if s == 0:
+                assert g == p

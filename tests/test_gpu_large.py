@@ -1,0 +1,106 @@
+"""GPU parity for values far above 64 KiB, up to BodyMax (50 MiB, config/mc_config.go:8):
+the general kernels k_encode_lane (values > 64 KiB) and k_dec_lane8 (dsize > 64 KiB) against
+the oracle, including long literal runs (the byte-serial loop of k_dec_lane8) and corrupted
+streams of such values.  Offsets >= 131071 (quicklz.c:361 falls back to literals) occur at
+these sizes."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+MIB = 1 << 20
+
+
+def _noisy(seed: int, n: int, p: float) -> bytes:
+    """Text with a fraction p of bytes replaced by random ones: compressed blocks full of
+    literal runs (compressible enough to stay compressed at p ~ 0.3)."""
+    t = np.frombuffer(O.gen_text(seed, 1, n), np.uint8).copy()
+    rng = np.random.default_rng(seed)
+    m = rng.random(n) < p
+    t[m] = rng.integers(0, 256, int(m.sum()), dtype=np.uint8)
+    return t.tobytes()
+
+
+def _values():
+    return {
+        "text_1MiB": O.gen_text(21, 0, 1 * MIB),
+        "noisy_8MiB": _noisy(22, 8 * MIB, 0.3),
+        "mixed_50MiB": O.gen_text(23, 0, 20 * MIB) + bytes(10 * MIB) + _noisy(24, 20 * MIB, 0.25),
+    }
+
+
+@pytest.fixture(scope="module")
+def large():
+    vals = _values()
+    return {k: (v, O.compress(v)) for k, v in vals.items()}
+
+
+def test_large_decode_matches_oracle(cuda, large):
+    """Oracle-compressed values through k_dec_lane8 (and the batch API's max_dsize routing)."""
+    import torch
+    from gobeansdb_amd import batch
+    names = list(large)
+    comp = [large[k][1] for k in names]
+    src = batch.BlockBatch.from_bytes(comp)
+    sizes = [len(large[k][0]) for k in names]
+    out = batch.BlockBatch.empty_for(sizes)
+    dsz, st, crc = batch.decompress(src, out, max_dsize=max(sizes), want_crc=True,
+                                    crc_state=torch.full((len(names),), -1, dtype=torch.int32, device="cuda"))
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().tolist() == [0] * len(names)
+    got = out.to_bytes(dsz.cpu().numpy())
+    for k, g in zip(names, got):
+        assert g == large[k][0], k
+    # fused record CRC over the compressed value == CRC of the compressed bytes
+    for k, c in zip(names, crc.cpu().numpy().view(np.uint32)):
+        assert int(c) == O.crc32_write(0xFFFFFFFF, large[k][1]) ^ 0xFFFFFFFF, k
+
+
+def test_large_encode_matches_oracle(cuda, large):
+    """k_encode_lane output bytes == the oracle (== reference quicklz.c) for 1 MiB and 8 MiB;
+    the 50 MiB value is compressed on the GPU and round-tripped through the oracle decoder."""
+    import torch
+    from gobeansdb_amd import batch
+    names = ["text_1MiB", "noisy_8MiB", "mixed_50MiB"]
+    src = batch.BlockBatch.from_bytes([large[k][0] for k in names])
+    dst, cs, st, _ = batch.compress(src, max_len=max(len(large[k][0]) for k in names))
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().tolist() == [0] * len(names)
+    outs = dst.to_bytes(cs.cpu().numpy())
+    for k, o in zip(names, outs):
+        assert o == large[k][1], k
+
+
+def test_large_corrupt_status_matches_oracle(cuda, large):
+    """Corrupted control words, tokens and literal bytes, and truncations, of the 1 MiB and
+    8 MiB streams: the GPU status (and output when OK) equals the oracle's."""
+    import torch
+    from gobeansdb_amd import batch
+    rng = np.random.default_rng(7)
+    cases = []
+    for k in ("text_1MiB", "noisy_8MiB"):
+        c = large[k][1]
+        for _ in range(6):
+            b = bytearray(c)
+            pos = int(rng.integers(9, len(b)))
+            b[pos] ^= int(rng.integers(1, 256))
+            cases.append(bytes(b))
+        b = bytearray(c)
+        b[-1] ^= 0x5A                    # last literal byte
+        cases.append(bytes(b))
+        cases.append(c[: len(c) // 2])   # truncated: csize mismatch
+    caps = [len(large["noisy_8MiB"][0])] * len(cases)
+    src = batch.BlockBatch.from_bytes(cases)
+    out = batch.BlockBatch.empty_for(caps)
+    cap_t = torch.tensor(np.asarray(caps, np.uint32).view(np.int32), device="cuda")
+    dsz, st, _ = batch.decompress(src, out, dst_cap=cap_t, max_dsize=max(caps))
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    got = out.to_bytes(dsz.cpu().numpy())
+    for c, cap, s, g in zip(cases, caps, st, got):
+        ost, od = O.decompress(c, cap=cap)
+        assert int(s) == ost
+        if ost == 0:
+            assert g == od

@@ -3,9 +3,10 @@
 
 A chunk file (store/datafile.go layout: 24-B header, key, value, 256-B padding)
 of --chunk-mib MiB is built once from synthetic values (log-uniform 4-64 KiB,
-70 % text / 30 % image-like).  Values pass a simplified TryCompress policy
-(store/item.go:145: keep the compressed body when float32(clen)/float32(len) <= 0.7;
-the 10 KiB trial and the MIME sniff are not modelled here).  Keys are "key_%016x".
+70 % text / 30 % image-like).  Values pass the TryCompress policy of store/item.go:120-161:
+the MIME sniff of the first 512 B (gobeansdb_amd.record.need_compress), a trial compress
+of the first 10 KiB kept when float32(clen)/float32(tlen) <= 0.7, then the whole body.
+Keys are "key_%016x".
 --files copies of that chunk (13 x 4000 MiB ~ 50 GiB by default) are replayed:
 
   device-only   the chunk is resident in HBM; one step = qlzx_replay_index +
@@ -30,6 +31,8 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
+
+from gobeansdb_amd.record import COMPRESS_RATIO_LIMIT, TRY_COMPRESS_SIZE, need_compress  # noqa: E402
 
 
 def log(*a):
@@ -62,12 +65,19 @@ def build_chunk(mib: int, seed: int, dev):
             ln = [sizes[i] for i in ids]
             plain = batch.synth(kind, seed, ln, first_id=int(ids[0]) * 7919, device=dev)
             comp, cs, st, _ = batch.compress(plain, max_len=max(ln))
+            tl = [min(n, TRY_COMPRESS_SIZE) for n in ln]   # store/item.go:133-140: the 10 KiB trial
+            trial = batch.BlockBatch(plain.data, plain.off, torch.tensor(tl, dtype=torch.int32, device=dev))
+            _, tcs, tst, _ = batch.compress(trial, max_len=max(tl))
             torch.cuda.synchronize()
+            assert int((st != 0).sum()) == 0 and int((tst != 0).sum()) == 0
             ph = plain.to_bytes()
             ch = comp.to_bytes(cs)
+            tcs_h = tcs.cpu().numpy()
             for j, i in enumerate(ids):
-                # TryCompress keep rule (store/item.go:145), float32 ratio
-                if np.float32(len(ch[j])) / np.float32(len(ph[j])) <= np.float32(0.7):
+                # TryCompress (store/item.go:137-156): sniff, float32 trial ratio, whole body
+                keep = need_compress(ph[j][:512]) and \
+                    np.float32(tcs_h[j]) / np.float32(tl[j]) <= np.float32(COMPRESS_RATIO_LIMIT)
+                if keep:
                     values[i], flags[i] = ch[j], 0x10000
                 else:
                     values[i] = ph[j]
@@ -99,7 +109,7 @@ def build_chunk(mib: int, seed: int, dev):
     for o, v in zip(rec_off, c):
         buf[o: o + 4] = np.frombuffer(struct.pack("<I", int(v)), np.uint8)
     del d
-    return buf, nrec, int(sum(len(v) for v in values[:nrec])), int(sum(sizes[:nrec]))
+    return buf, nrec, int(sum(len(v) for v in values[:nrec])), int(sum(sizes[:nrec])), np.asarray(rec_off, np.uint64)
 
 
 def main():
@@ -108,11 +118,13 @@ def main():
     p.add_argument("--files", type=int, default=13)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--seed", type=int, default=2026)
+    p.add_argument("--cpu-seconds", type=float, default=8.0)
+    p.add_argument("--no-cpu", action="store_true")
     a = p.parse_args()
     from gobeansdb_amd import replay, batch
     dev = torch.device("cuda", 0)
     t0 = time.time()
-    host, nrec, stored_bytes, raw_bytes = build_chunk(a.chunk_mib, a.seed, dev)
+    host, nrec, stored_bytes, raw_bytes, rec_off = build_chunk(a.chunk_mib, a.seed, dev)
     log(f"chunk built in {time.time() - t0:.1f}s: {len(host) / 2**20:.0f} MiB, {nrec} records")
     pinned = torch.from_numpy(host).pin_memory()
     dchunk = pinned.to(dev, non_blocking=False)
@@ -184,6 +196,7 @@ def main():
     torch.cuda.synchronize()
     pipe_s = time.perf_counter() - t
     chunk_gib = len(host) / 2**30
+    cpu = None if a.no_cpu else cpu_baseline(host, rec_off, a.cpu_seconds)
     rec = {
         "metric": "GiB/s .data replay (record scan + CRC + decompress + vhash), c4",
         "chunk_mib": a.chunk_mib, "records_per_chunk": nrec,
@@ -200,8 +213,53 @@ def main():
                                  "note": "H2D of file i+1, replay of file i and D2H of file i-1 on three streams, "
                                          "two device chunk slots, two pinned output slots"},
         "data": "synthetic",
+        "cpu_baseline": cpu,
     }
     print(json.dumps(rec), flush=True)
+
+
+def cpu_baseline(host: np.ndarray, rec_off: np.ndarray, seconds: float):
+    """The reference record loop (store/bucket.go:89-117 over store/datafile.go:228-277) on the
+    host cores over the same chunk: CRC verify with the reference crc32_write, the reference
+    qlz_decompress for FLAG_COMPRESS values, Getvhash (oracle/qlz_oracle.c orc_bench_replay,
+    reference code from oracle/_ref).  Records are split into contiguous ranges, one per
+    thread (buckets replay independently in the reference)."""
+    import ctypes
+    from bench import host_cpus
+    from oracle import oracle as O
+    Q, C = O.ref_if_built(), O.crc_ref_if_built()
+    if Q is None or C is None:
+        return None
+    L = O.lib()
+    threads, nproc, model = host_cpus()
+    dec = ctypes.cast(Q.qlz_decompress, ctypes.c_void_p).value
+    crc = ctypes.cast(C.crc32_write, ctypes.c_void_p).value
+    bad = ctypes.c_uint64(0)
+
+    def run(nthr, nbytes_cap, secs, cgo):
+        n = len(rec_off)
+        # records [0, last): all of them, or those starting before the byte cap
+        last = n if nbytes_cap is None else max(1, int(np.searchsorted(rec_off, nbytes_cap, side="left")))
+        end = len(host) if last == n else int(rec_off[last])
+        cuts = np.asarray([int(rec_off[last * t // nthr]) for t in range(nthr)] + [end], np.uint64)
+        span = int(cuts[-1] - cuts[0])
+        reps, ns = 0, 0.0
+        t_end = time.time() + secs
+        while time.time() < t_end or reps == 0:
+            ns += L.orc_bench_replay(dec, crc, host.ctypes.data, cuts.ctypes.data, nthr, int(cgo), ctypes.byref(bad))
+            reps += 1
+            if bad.value:
+                raise RuntimeError(f"reference replay: {bad.value} records failed CRC/decompress")
+        return reps * span / (ns * 1e-9) / 2**30, reps, span
+
+    gibs, reps, span = run(threads, None, seconds, True)
+    one, _, one_span = run(1, 256 << 20, max(2.0, seconds / 4), True)
+    return {"value": round(gibs, 3), "unit": "GiB/s of chunk", "cores": threads, "kind": "reference",
+            "sample": f"{reps} passes over the whole {span / 2**20:.0f} MiB chunk, {threads} threads on contiguous "
+                      f"record ranges; per record: reference crc32_write over header[4:24]|key|value, "
+                      f"reference qlz_decompress (output malloc per value, cgo-faithful) if FLAG_COMPRESS, Getvhash",
+            "threads": threads, "nproc": nproc, "cpu_model": model, "one_core": round(one, 3),
+            "one_core_sample": f"first {one_span / 2**20:.0f} MiB of the chunk"}
 
 
 if __name__ == "__main__":

@@ -1,0 +1,93 @@
+"""Per-call latency of the single-call drop-ins (qlz_compress, qlz_decompress, crc32_write)
+against the reference C build (oracle/_ref) called the same way, one call at a time.
+
+These are the calls store/ makes per value: CCompress once or twice per set
+(store/item.go:140,151), crc32.write three times per record (store/datafile.go:68-74),
+CDecompressSafe per get (store/item.go:167).  Every call goes through ctypes on both sides,
+so the Python call overhead (~1 us) is in both columns.  The reference column "cgo" also
+allocates a 528,400-B scratch and the output buffer per call, as cquicklz.go:24-34 does.
+
+usage: python tools/bench_single.py [--calls 300] [--out profiles/r02_single_call.json]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def med_us(fn, calls):
+    ts = []
+    for _ in range(calls):
+        t0 = time.perf_counter_ns()
+        fn()
+        ts.append(time.perf_counter_ns() - t0)
+    return round(float(np.median(ts)) / 1e3, 2)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--calls", type=int, default=300)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    from gobeansdb_amd import _lib
+    from oracle import oracle as O
+    L = _lib.lib()
+    ref = O.ref()
+    rows = []
+    for n in (4096, 16384, 65536):
+        plain = O.gen_text(0x5EED2026, n, n)
+        comp = O.compress(plain)
+        src = np.frombuffer(plain, np.uint8).copy()
+        csrc = np.frombuffer(comp, np.uint8).copy()
+        dst = np.zeros(n + 400, np.uint8)
+        scratch = np.zeros(528400, np.uint8)
+        # correctness of both sides before timing
+        assert L.qlz_compress(src.ctypes.data, dst.ctypes.data, n, scratch.ctypes.data) == len(comp)
+        assert dst[:len(comp)].tobytes() == comp
+        assert L.qlz_decompress(csrc.ctypes.data, dst.ctypes.data, scratch.ctypes.data) == n
+        assert dst[:n].tobytes() == plain
+        assert L.crc32_write(0xFFFFFFFF, src.ctypes.data, n) == O.crc32_write(0xFFFFFFFF, plain)
+        row = {"bytes": n, "ratio": round(len(comp) / n, 3)}
+        row["gpu_compress_us"] = med_us(lambda: L.qlz_compress(src.ctypes.data, dst.ctypes.data, n, 0), a.calls)
+        row["gpu_decompress_us"] = med_us(lambda: L.qlz_decompress(csrc.ctypes.data, dst.ctypes.data, 0), a.calls)
+        row["gpu_crc32_us"] = med_us(lambda: L.crc32_write(0xFFFFFFFF, src.ctypes.data, n), a.calls)
+        if ref is not None:
+            Q, C = ref
+
+            def cgo_compress():
+                sc = np.empty(528400, np.uint8)
+                out = np.empty(n + 400, np.uint8)
+                Q.qlz_compress(src.ctypes.data, out.ctypes.data, n, sc.ctypes.data)
+
+            def cgo_decompress():
+                out = np.empty(n, np.uint8)
+                Q.qlz_decompress(csrc.ctypes.data, out.ctypes.data, scratch.ctypes.data)
+
+            row["ref_compress_us"] = med_us(lambda: Q.qlz_compress(src.ctypes.data, dst.ctypes.data, n,
+                                                                   scratch.ctypes.data), a.calls)
+            row["ref_compress_cgo_us"] = med_us(cgo_compress, a.calls)
+            row["ref_decompress_us"] = med_us(lambda: Q.qlz_decompress(csrc.ctypes.data, dst.ctypes.data,
+                                                                       scratch.ctypes.data), a.calls)
+            row["ref_decompress_cgo_us"] = med_us(cgo_decompress, a.calls)
+            row["ref_crc32_us"] = med_us(lambda: C.crc32_write(0xFFFFFFFF, src.ctypes.data, n), a.calls)
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    res = {"what": "median per-call latency, one call at a time (ctypes on both sides), text values",
+           "calls_per_point": a.calls, "rows": rows,
+           "reference": "oracle/_ref (quicklz.c, crc32.go preamble; gcc -O2)" if ref else None}
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
