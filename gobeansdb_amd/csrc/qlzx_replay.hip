@@ -29,53 +29,133 @@ enum : uint8_t { kSlotBadSize = 1, kSlotTrunc = 2, kSlotPartial = 3, kSlotCand =
 constexpr uint32_t kScanTile = 1024;  // elements per scan tile (256 threads x 4)
 
 struct RpCounters {
-    uint32_t ncand, m, r0, nvis, end_kind, pad[3];
+    uint32_t ncand, m, r0, nvis, end_kind, nlong, pad[2];
 };
-
-__device__ __forceinline__ uint32_t ld32u(const uint8_t *p) {
-    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
 
 // 1. slot classification (readRecordAt's size checks, store/datafile.go:128-136)
 __global__ void __launch_bounds__(256) k_rp_slots(const uint8_t *data, uint64_t size, uint32_t nslots,
                                                   uint32_t max_key, uint64_t body_max, uint8_t *kind,
                                                   uint32_t *rsz, uint32_t *cand, RpCounters *cnt) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nslots) return;
+    const bool in = s < nslots;
     const uint64_t off = (uint64_t)s * kRpSlot;
-    rsz[s] = 0;
-    uint8_t k;
-    if (off + kRpHdr > size) {
-        k = kSlotPartial;
-    } else {
-        const uint8_t *h = data + off;
-        const uint32_t ksz = ld32u(h + 16), vsz = ld32u(h + 20);
+    uint8_t k = kSlotPartial;
+    if (in && off + kRpHdr <= size) {
+        // slots are 256-B aligned in the chunk: two aligned dword loads (ksz, vsz)
+        const uint2 kv = *(const uint2 *)(data + off + 16);
+        const uint32_t ksz = kv.x, vsz = kv.y;
         if (ksz == 0 || ksz > max_key || (uint64_t)vsz > body_max) k = kSlotBadSize;
         else if (off + kRpHdr + ksz + vsz > size) k = kSlotTrunc;
         else k = kSlotCand;
     }
-    kind[s] = k;
-    if (k == kSlotCand) cand[atomicAdd(&cnt->ncand, 1u)] = s;
+    if (in) {
+        rsz[s] = 0;
+        kind[s] = k;
+    }
+    // candidates: one counter atomic per wave (ballot + rank), not per slot
+    const uint64_t m = __ballot(in && k == kSlotCand);
+    if (m) {
+        const uint32_t lane = threadIdx.x & 63;
+        const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&cnt->ncand, (uint32_t)__builtin_popcountll(m));
+        base = __shfl(base, leader, 64);
+        if (in && k == kSlotCand)
+            cand[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = s;
+    }
 }
 
-// 2. record CRC of every candidate, one wave each (wave_crc_raw of qlzx_crc.hip)
-__device__ uint32_t wave_crc_raw(const uint32_t *tab, const uint8_t *p, uint64_t len, uint32_t lane);
+// 2. record CRC of every candidate, one wave each (wave_crc of qlzx_crc.hip).  A wave
+// takes ~3 us per 4 KiB stripe, so a candidate longer than kRpLong (a false candidate can
+// claim up to BodyMax = 50 MiB) would be one wave's serial tail for the whole launch: those go
+// to a list (lng[], their per-list XOR accumulator and segment counter zeroed here) and are
+// cut into kRpSeg segments that k_rp_crc_long spreads over every wave of the chip.
+constexpr uint32_t kRpLong = 128u << 10;
+constexpr uint32_t kRpSeg = 16u << 10;
+
+__device__ __forceinline__ void rp_crc_verdict(const uint8_t *h, uint32_t s, uint32_t ksz, uint32_t vsz,
+                                               uint32_t reg, uint32_t *rsz) {
+    if ((reg ^ 0xffffffffu) == *(const uint32_t *)h) rsz[s] = ((kRpHdr + ksz + vsz + 255u) >> 8) << 8;
+}
 
 __global__ void __launch_bounds__(256) k_rp_crc(const uint8_t *data, const uint32_t *cand,
-                                                const RpCounters *cnt, uint32_t *rsz) {
-    __shared__ uint32_t tab[8 * 256];
-    load_crc_slice8(tab);
+                                                RpCounters *cnt, uint32_t *rsz, uint32_t *lng,
+                                                uint32_t *lacc, uint32_t *ldone) {
+    __shared__ uint32_t tab[kCrcLdsWords];
+    load_crc_lds(tab);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nc = cnt->ncand;
     for (uint32_t c = blockIdx.x * 4 + threadIdx.x / 64; c < nc; c += gridDim.x * 4) {
         const uint32_t s = cand[c];
         const uint8_t *h = data + (uint64_t)s * kRpSlot;
-        const uint32_t ksz = ld32u(h + 16), vsz = ld32u(h + 20);
-        const uint32_t len = 20 + ksz + vsz;  // header[4:24] ‖ key ‖ value
-        const uint32_t raw = wave_crc_raw(tab, h + 4, len, lane);
-        const uint32_t crc = (raw ^ crc_shift(0xffffffffu, len)) ^ 0xffffffffu;
-        if (lane == 0 && crc == ld32u(h)) rsz[s] = ((kRpHdr + ksz + vsz + 255u) >> 8) << 8;
+        const uint2 kv = *(const uint2 *)(h + 16);
+        const uint32_t len = 20 + kv.x + kv.y;  // header[4:24] ‖ key ‖ value
+        if (len > kRpLong) {
+            if (lane == 0) {
+                const uint32_t j = atomicAdd(&cnt->nlong, 1u);
+                lng[j] = s;
+                lacc[j] = 0;
+                ldone[j] = 0;
+            }
+            continue;
+        }
+        const uint32_t reg = wave_crc(tab, h + 4, len, 0xffffffffu, lane);
+        if (lane == 0) rp_crc_verdict(h, s, kv.x, kv.y, reg, rsz);
+    }
+}
+
+// long candidates: every wave walks the (normally empty or tiny) list 64 entries at a time
+// (one load per lane, a wave scan of the segment counts) and takes the segments g of the
+// global segment sequence with g = wave id (mod all waves).  A segment's raw CRC, shifted over
+// the bytes after it, is XORed into its candidate's accumulator, and the wave that completes
+// the last segment (counter == nseg) turns the sum into the verdict.
+__global__ void __launch_bounds__(256) k_rp_crc_long(const uint8_t *data, const RpCounters *cnt,
+                                                     uint32_t *rsz, const uint32_t *lng, uint32_t *lacc,
+                                                     uint32_t *ldone) {
+    __shared__ uint32_t tab[kCrcLdsWords];
+    const uint32_t nl = cnt->nlong;
+    if (nl == 0) return;
+    load_crc_lds(tab);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = blockIdx.x * 4 + threadIdx.x / 64, nw = gridDim.x * 4;
+    uint64_t base = 0;  // global index of the batch's first segment
+    for (uint32_t e0 = 0; e0 < nl; e0 += 64) {
+        const uint32_t e = e0 + lane;
+        uint32_t s = 0, len = 0;
+        if (e < nl) {
+            s = lng[e];
+            const uint2 kv = *(const uint2 *)(data + (uint64_t)s * kRpSlot + 16);
+            len = 20 + kv.x + kv.y;
+        }
+        const uint32_t ns = (len + kRpSeg - 1) / kRpSeg;
+        uint32_t inc = ns;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d, 64);
+            if (lane >= (uint32_t)d) inc += y;
+        }
+        const uint32_t total = __shfl(inc, 63, 64);
+        for (uint32_t r = (uint32_t)((wid + nw - base % nw) % nw); r < total; r += nw) {
+            const uint32_t L = (uint32_t)__builtin_ctzll(__ballot(inc > r));
+            const uint32_t sl_s = __shfl(s, L, 64), sl_len = __shfl(len, L, 64);
+            const uint32_t nseg = __shfl(ns, L, 64);
+            const uint32_t o = (r - (__shfl(inc, L, 64) - nseg)) * kRpSeg;
+            const uint32_t sl = sl_len - o < kRpSeg ? sl_len - o : kRpSeg;
+            const uint8_t *h = data + (uint64_t)sl_s * kRpSlot;
+            // segment 0 carries the initial state; each register is shifted over the rest
+            const uint32_t raw = crc_shift(wave_crc(tab, h + 4 + o, sl, o ? 0u : 0xffffffffu, lane), sl_len - o - sl);
+            if (lane == 0) {
+                atomicXor(&lacc[e0 + L], raw);
+                __threadfence();
+                if (atomicAdd(&ldone[e0 + L], 1u) == nseg - 1) {
+                    __threadfence();
+                    const uint2 kv = *(const uint2 *)(h + 16);
+                    rp_crc_verdict(h, sl_s, kv.x, kv.y, atomicOr(&lacc[e0 + L], 0u), rsz);
+                }
+            }
+        }
+        base += total;
     }
 }
 
@@ -312,8 +392,11 @@ inline int launch_replay_index(const uint8_t *data, uint64_t size, uint64_t star
     if (nslots)
         hipLaunchKernelGGL(k_rp_slots, dim3((nslots + 255) / 256), dim3(256), 0, s, data, size, nslots, max_key,
                            body_max, w.kind, w.rsz, w.cand, w.cnt);
-    const uint32_t crc_grid = nslots / 4 + 1 < 65536 ? nslots / 4 + 1 : 65536;
-    hipLaunchKernelGGL(k_rp_crc, dim3(crc_grid), dim3(256), 0, s, data, w.cand, w.cnt, w.rsz);
+    // a grid-stride loop over the candidates: one table load per workgroup, 8 per CU
+    const uint32_t crc_grid = nslots / 4 + 1 < 2048 ? nslots / 4 + 1 : 2048;
+    // the long-candidate list and its accumulators borrow vis, J and J2 (written later)
+    hipLaunchKernelGGL(k_rp_crc, dim3(crc_grid), dim3(256), 0, s, data, w.cand, w.cnt, w.rsz, w.vis, w.J, w.J2);
+    hipLaunchKernelGGL(k_rp_crc_long, dim3(2048), dim3(256), 0, s, data, w.cnt, w.rsz, w.vis, w.J, w.J2);
     // valid slots in order: vidx (exclusive count) and A
     ValidFlag vf{w.rsz};
     hipLaunchKernelGGL(k_scan_tiles<ValidFlag>, dim3(ntiles), dim3(256), 0, s, vf, nslots, w.tiles);

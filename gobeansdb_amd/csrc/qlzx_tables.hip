@@ -101,6 +101,48 @@ __device__ uint32_t g_crc_stripe[64] = {T64(stripe)};
 #undef T64
 #undef T8
 
+// Multiply-by-constant tables for wave_crc: g_crc_mul[i * 1024 + j * 256 + b] = (b << 8 j) *
+// x^(8 kMulBytes[i]) mod P, so a register c times that power is four lookups, one per byte.
+// i = 0..5: 64 * 2^i bytes (the lane-combine tree), i = 6: 4032 bytes (the other 63 lanes'
+// pieces of a 4 KiB stripe).
+constexpr int kMulTabs = 7;
+struct CrcMul {
+    uint32_t t[kMulTabs * 1024];
+};
+__host__ __device__ constexpr CrcMul make_mul() {
+    CrcMul m{};
+    const uint32_t pieces[kMulTabs] = {1, 2, 4, 8, 16, 32, 63};
+    for (int i = 0; i < kMulTabs; i++) {
+        const uint32_t k = kTables.piece[pieces[i]];
+        // b -> (b << 8 j) * k is linear in b: build from the 8 single-bit products
+        for (int j = 0; j < 4; j++) {
+            uint32_t bit[8] = {};
+            for (int q = 0; q < 8; q++) bit[q] = mulmod_c(k, 1u << (8 * j + q));
+            for (uint32_t b = 0; b < 256; b++) {
+                uint32_t v = 0;
+                for (int q = 0; q < 8; q++)
+                    if (b & (1u << q)) v ^= bit[q];
+                m.t[i * 1024 + j * 256 + b] = v;
+            }
+        }
+    }
+    return m;
+}
+constexpr CrcMul kMul = make_mul();
+static_assert(kMul.t[0] == 0 && kMul.t[6 * 1024 + 256 + 1] == mulmod_c(kTables.piece[63], 1u << 8), "crc mul");
+
+#define M8(i) kMul.t[i], kMul.t[i + 1], kMul.t[i + 2], kMul.t[i + 3], kMul.t[i + 4], kMul.t[i + 5], \
+    kMul.t[i + 6], kMul.t[i + 7]
+#define M64(i) M8(i), M8(i + 8), M8(i + 16), M8(i + 24), M8(i + 32), M8(i + 40), M8(i + 48), M8(i + 56)
+#define M1K(i) M64(i), M64(i + 64), M64(i + 128), M64(i + 192), M64(i + 256), M64(i + 320), M64(i + 384), \
+    M64(i + 448), M64(i + 512), M64(i + 576), M64(i + 640), M64(i + 704), M64(i + 768), M64(i + 832), \
+    M64(i + 896), M64(i + 960)
+__device__ uint32_t g_crc_mul[kMulTabs * 1024] = {M1K(0), M1K(1024), M1K(2048), M1K(3072), M1K(4096),
+                                                  M1K(5120), M1K(6144)};
+#undef M1K
+#undef M64
+#undef M8
+
 }  // namespace qlzx
 
 // Host copies (used by the single-call crc32_write path's self-check and tests).

@@ -144,6 +144,31 @@ def test_crc_batch(cuda, golden):
         assert int(c) == O.crc32_write(0x12345678, d)
 
 
+def test_crc_unaligned_and_stripe_edges(cuda):
+    """wave_crc: every length 0..300 and the 4 KiB stripe edges (4095/4096/4097, 8191, ...,
+    1 MiB + 3) at every start alignment 0..3 of one shared buffer, with a non-default init."""
+    import torch
+    from gobeansdb_amd import batch
+    rng = np.random.default_rng(3)
+    buf = rng.integers(0, 256, (2 << 20) + 64, dtype=np.uint8)
+    lens = list(range(0, 301)) + [4092, 4095, 4096, 4097, 4100, 8191, 8192, 8193, 12345, 65536 + 7, (1 << 20) + 3]
+    offs, ls = [], []
+    for k, n in enumerate(lens):
+        for m in range(4):
+            offs.append(8 * k + m)
+            ls.append(n)
+    d = torch.from_numpy(buf).cuda()
+    src = batch.BlockBatch(d, torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                           torch.tensor(ls, dtype=torch.int32, device="cuda"))
+    init = torch.tensor(np.full(len(ls), 0x9E3779B9, np.uint32).view(np.int32), device="cuda")
+    got = batch.crc32(src, init=init, final_xor=0).cpu().numpy().view(np.uint32)
+    std = batch.crc32(src).cpu().numpy().view(np.uint32)
+    for o, n, g, s in zip(offs, ls, got, std):
+        b = buf[o:o + n].tobytes()
+        assert int(g) == O.crc32_write(0x9E3779B9, b), (o, n)
+        assert int(s) == zlib.crc32(b), (o, n)
+
+
 @pytest.mark.parametrize("kind", ["text", "image"])
 def test_synth_matches_oracle(cuda, kind):
     import torch

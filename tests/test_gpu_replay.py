@@ -109,3 +109,33 @@ def test_start_offset_and_edges(cuda):
     _check(b"")
     _check(bytes(4096))                     # all zero: no record, clean end
     _check(bytes(100))                      # partial header
+
+
+def test_long_candidates(cuda):
+    """Records and false candidates longer than the replay's single-wave CRC limit (128 KiB):
+    their CRC is cut into 64 KiB segments over many waves (k_rp_crc_long).  A 3 MiB raw record
+    embeds, on slot boundaries, a valid 2 MiB record and a header with valid sizes but a wrong
+    CRC (a 1.5 MiB false candidate); a 1 MiB compressed record follows.  Intact, the reader
+    never sees the embedded ones; with the outer record's CRC broken it resyncs into them."""
+    rng = np.random.default_rng(11)
+    emb = R.make_record(b"embedded", rng.integers(0, 256, 2 << 20, dtype=np.uint8).tobytes(), ver=3)
+    fake = bytearray(R.make_record(b"fake_key", bytes(1536 << 10)))
+    fake[0] ^= 0xFF                                     # wrong CRC, sizes intact
+    key = b"outer"
+    lead = 4096 - 24 - len(key)                         # embedded record at file offset 4096
+    body = rng.integers(0, 256, lead, dtype=np.uint8).tobytes() + emb
+    body += rng.integers(0, 256, (-(24 + len(key) + len(body))) % 256 + 512, dtype=np.uint8).tobytes()
+    body += bytes(fake[:24 + 8])                        # the fake header + key, on a slot boundary
+    body += rng.integers(0, 256, (3 << 20) - len(body), dtype=np.uint8).tobytes()
+    outer = bytearray(R.make_record(key, body))
+    text = O.gen_text(5, 0, 1 << 20)
+    tail = R.make_record(b"text_1MiB", O.compress(text), flag=R.FLAG_COMPRESS)
+    data = bytes(outer) + tail
+    rows, err = _gpu(data)
+    assert [r[2] for r in rows] == [key, b"text_1MiB"] and rows[1][5] == text and not err
+    _check(data)
+    outer[24 + len(key) + 7] ^= 1                       # outer CRC now wrong: resync inside it
+    data = bytes(outer) + tail
+    rows, _ = _gpu(data)
+    assert rows[0][0] == 4096 and rows[0][2] == b"embedded"
+    _check(data)
