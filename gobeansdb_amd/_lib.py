@@ -23,6 +23,7 @@ STATUS_NAMES = ["OK", "E_SIZE_COMPRESSED", "E_CORRUPT", "E_LEVEL", "E_DST_CAP", 
 
 
 F_GO_COMPAT = 1
+F_LEVEL1 = 2
 
 
 class QlzxError(RuntimeError):
@@ -76,6 +77,14 @@ def lib() -> ctypes.CDLL:
     L.qlzx_compress_batch.restype = ctypes.c_int
     L.qlzx_compress1.argtypes = [vp, vp, sz, u32]
     L.qlzx_compress1.restype = sz
+    L.qlzx_go_l1_workspace_size.argtypes = [u32]
+    L.qlzx_go_l1_workspace_size.restype = sz
+    L.qlzx_go_l1_compress_batch.argtypes = [BP, vp, vp, vp, sz, vp]
+    L.qlzx_go_l1_compress_batch.restype = ctypes.c_int
+    L.qlzx_go_decompress_batch.argtypes = [BP, vp, vp, vp, vp, sz, vp]
+    L.qlzx_go_decompress_batch.restype = ctypes.c_int
+    L.qlzx_go_decompress1.argtypes = [vp, sz, vp, sz]
+    L.qlzx_go_decompress1.restype = sz
     L.qlzx_crc32_batch.argtypes = [vp, vp, vp, u32, vp, u32, vp, vp]
     L.qlzx_crc32_batch.restype = ctypes.c_int
     L.qlzx_synth_batch.argtypes = [ctypes.c_int, u64, u64, vp, vp, vp, u32, vp, vp, vp, u32, vp]

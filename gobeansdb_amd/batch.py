@@ -147,6 +147,44 @@ def compress(src: BlockBatch, dst: BlockBatch | None = None, *, crc_state: torch
     return dst, csize, status, crc_out
 
 
+def go_l1_compress(src: BlockBatch, dst: BlockBatch | None = None, workspace: Workspace | None = None,
+                   stream=None):
+    """Batch Go quicklz.Compress(src, 1) (quicklz.go:80-191), one lane per block.
+    Returns (dst BlockBatch, csize i32, status i32)."""
+    L = _lib.lib()
+    n = src.n
+    dev = src.data.device
+    if dst is None:
+        dst = BlockBatch.empty_for(src.length.cpu().numpy().view(np.uint32), device=dev, pad=400)
+    csize = torch.zeros(n, dtype=torch.int32, device=dev)
+    status = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    ws_bytes = L.qlzx_go_l1_workspace_size(n)
+    ws = (workspace or Workspace(dev)).get(ws_bytes)
+    b = _blocks(src, dst.data, dst.off)
+    rc = L.qlzx_go_l1_compress_batch(ctypes.byref(b), csize.data_ptr(), status.data_ptr(), ws.data_ptr(),
+                                     ws_bytes, _stream(stream))
+    _lib.check(rc, "qlzx_go_l1_compress_batch")
+    return dst, csize, status
+
+
+def go_decompress(src: BlockBatch, dst: BlockBatch, *, dst_cap: torch.Tensor | None = None,
+                  workspace: Workspace | None = None, stream=None):
+    """Batch Go quicklz.Decompress of stored and level-1 streams (quicklz.go:291-431),
+    one lane per block.  Returns (dsize i32, status i32)."""
+    L = _lib.lib()
+    n = src.n
+    dev = src.data.device
+    dsize = torch.zeros(n, dtype=torch.int32, device=dev)
+    status = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    ws_bytes = L.qlzx_go_l1_workspace_size(n)
+    ws = (workspace or Workspace(dev)).get(ws_bytes)
+    b = _blocks(src, dst.data, dst.off)
+    rc = L.qlzx_go_decompress_batch(ctypes.byref(b), _ptr(dst_cap), dsize.data_ptr(), status.data_ptr(),
+                                    ws.data_ptr(), ws_bytes, _stream(stream))
+    _lib.check(rc, "qlzx_go_decompress_batch")
+    return dsize, status
+
+
 def crc32(src: BlockBatch, init: torch.Tensor | None = None, final_xor: int = 0xFFFFFFFF, stream=None):
     """out[i] = crc32_write(init[i] or ~0, block i) ^ final_xor (store/crc32.go:61-88)."""
     L = _lib.lib()

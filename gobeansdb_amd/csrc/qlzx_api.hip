@@ -21,6 +21,7 @@
 #include "qlzx_encode_wg.hip"
 #include "qlzx_replay.hip"
 #include "qlzx_record.hip"
+#include "qlzx_level1.hip"
 
 namespace {
 
@@ -168,6 +169,38 @@ int qlzx_compress_batch(const qlzx_blocks *b, uint32_t *csize, int32_t *status,
                            crc_state, crc_out, (uint8_t *)workspace, nl, min_len, flags);
         HIP_OK(hipGetLastError());
     }
+    return QLZX_R_OK;
+}
+
+size_t qlzx_go_l1_workspace_size(uint32_t n) { return (size_t)n * qlzx::kL1WsBlock; }
+
+static int check_l1_args(const qlzx_blocks *b, const void *out, void *workspace, size_t workspace_bytes,
+                         const char *who) {
+    if (!b || !out) return fail(QLZX_R_BAD_ARG, who);
+    if (b->n == 0) return QLZX_R_OK;
+    if (!b->src || !b->src_off || !b->src_len || !b->dst || !b->dst_off) return fail(QLZX_R_BAD_ARG, who);
+    if (!workspace || (((uintptr_t)workspace) & 15u) || workspace_bytes < qlzx_go_l1_workspace_size(b->n))
+        return fail(QLZX_R_WORKSPACE, who);
+    return QLZX_R_OK;
+}
+
+int qlzx_go_l1_compress_batch(const qlzx_blocks *b, uint32_t *csize, int32_t *status, void *workspace,
+                              size_t workspace_bytes, void *stream) {
+    if (int r = check_l1_args(b, csize, workspace, workspace_bytes, "qlzx_go_l1_compress_batch")) return r;
+    if (b->n == 0) return QLZX_R_OK;
+    hipLaunchKernelGGL(qlzx::k_enc_go_l1, dim3((b->n + 63) / 64), dim3(64), 0, (hipStream_t)stream, *b, csize,
+                       status, (uint8_t *)workspace);
+    HIP_OK(hipGetLastError());
+    return QLZX_R_OK;
+}
+
+int qlzx_go_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_t *dsize, int32_t *status,
+                             void *workspace, size_t workspace_bytes, void *stream) {
+    if (int r = check_l1_args(b, status, workspace, workspace_bytes, "qlzx_go_decompress_batch")) return r;
+    if (b->n == 0) return QLZX_R_OK;
+    hipLaunchKernelGGL(qlzx::k_dec_go_l1, dim3((b->n + 63) / 64), dim3(64), 0, (hipStream_t)stream, *b, dst_cap,
+                       dsize, status, (uint8_t *)workspace);
+    HIP_OK(hipGetLastError());
     return QLZX_R_OK;
 }
 
@@ -320,8 +353,9 @@ size_t qlzx_compress1(const void *source, char *destination, size_t size, uint32
     if (size == 0 || size > 0xffffffffull - 400) return 0;  // quicklz.c:705-706
     Ctx &c = t_ctx;
     if (c.init()) return 0;
+    const bool l1 = (flags & QLZX_F_LEVEL1) != 0;
     const size_t src_b = align_up(size, 256), dst_b = align_up(size + 400, 256);
-    const size_t ws_b = qlzx_compress_workspace_size(1, (uint32_t)size);
+    const size_t ws_b = l1 ? qlzx_go_l1_workspace_size(1) : qlzx_compress_workspace_size(1, (uint32_t)size);
     // pinned: [meta | src staging, reused for the result]
     if (c.reserve(256 + src_b + dst_b + ws_b, 256 + std::max(src_b, dst_b))) return 0;
     uint8_t *d_meta = c.d_buf, *d_src = d_meta + 256, *d_dst = d_src + src_b, *d_ws = d_dst + dst_b;
@@ -334,8 +368,9 @@ size_t qlzx_compress1(const void *source, char *destination, size_t size, uint32
     if (hipMemcpyAsync(d_meta, c.h_buf, 256 + size, hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
     Meta *dm = (Meta *)d_meta;
     qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
-    if (qlzx_compress_batch(&b, &dm->out_size, &dm->status, nullptr, nullptr, (uint32_t)size, flags, d_ws,
-                            ws_b, c.s))
+    if (l1 ? qlzx_go_l1_compress_batch(&b, &dm->out_size, &dm->status, d_ws, ws_b, c.s)
+           : qlzx_compress_batch(&b, &dm->out_size, &dm->status, nullptr, nullptr, (uint32_t)size, flags, d_ws,
+                                 ws_b, c.s))
         return 0;
     // one D2H of descriptor + the largest possible result, then the only synchronisation
     if (hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
@@ -374,6 +409,43 @@ size_t qlz_decompress(const char *source, void *destination, char *scratch_decom
     if (m->status != QLZX_OK) return 0;
     memcpy(destination, h_data, dsize);
     return m->out_size;
+}
+
+size_t qlzx_go_decompress1(const char *source, size_t source_len, void *destination, size_t dst_cap) {
+    if (!source || source_len == 0) return 0;
+    const size_t hdr = (source[0] & 2) ? 9 : 3;
+    const size_t dsize = source_len >= hdr ? qlz_size_decompressed(source) : 0;  // else the kernel: E_HEADER
+    if (dsize > dst_cap) {
+        fail(QLZX_R_BAD_ARG, "qlzx_go_decompress1: destination too small");
+        return 0;
+    }
+    Ctx &c = t_ctx;
+    if (c.init()) return 0;
+    const size_t src_b = align_up(source_len, 256), dst_b = align_up(dsize + 1, 256);
+    const size_t ws_b = qlzx_go_l1_workspace_size(1);
+    if (c.reserve(256 + src_b + dst_b + ws_b, 256 + std::max(src_b, dst_b))) return 0;
+    uint8_t *d_meta = c.d_buf, *d_src = d_meta + 256, *d_dst = d_src + src_b, *d_ws = d_dst + dst_b;
+    Meta *m = (Meta *)c.h_buf;
+    uint8_t *h_data = c.h_buf + 256;
+    memset(m, 0, sizeof(Meta));
+    m->src_len = (uint32_t)source_len;
+    m->dst_cap = (uint32_t)dsize;
+    memcpy(h_data, source, source_len);
+    if (hipMemcpyAsync(d_meta, c.h_buf, 256 + source_len, hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
+    Meta *dm = (Meta *)d_meta;
+    qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
+    if (qlzx_go_decompress_batch(&b, &dm->dst_cap, &dm->out_size, &dm->status, d_ws, ws_b, c.s)) return 0;
+    if (hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
+    if (dsize && hipMemcpyAsync(h_data, d_dst, dsize, hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
+    if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
+    if (m->status != QLZX_OK) {
+        char msg[64];
+        snprintf(msg, sizeof msg, "qlzx_go_decompress1: status %d", (int)m->status);
+        fail(QLZX_R_BAD_ARG, msg);
+        return 0;
+    }
+    memcpy(destination, h_data, dsize);
+    return dsize ? dsize : 0;
 }
 
 uint32_t crc32_write(uint32_t crc, unsigned char *buf, int len) {

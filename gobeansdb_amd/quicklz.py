@@ -103,33 +103,37 @@ def CDecompressSafe(src) -> tuple[CArray, QuicklzError | None]:
 def Compress(source, level: int) -> bytes | None:
     """quicklz.go:80-289: Go encoder.  Level 3 differs from CCompress in three
     ways (always a 9-byte header, earlier bail-out, nil on empty), reproduced
-    by the GPU encoder's GO_COMPAT mode.  Level 1 is not built."""
+    by the GPU encoder's GO_COMPAT mode; level 1 (quicklz.go:120-191) is the
+    lane-per-block k_enc_go_l1 (qlzx_level1.hip)."""
     if level not in (1, 3):
         raise QuicklzError("Go version only supports level 1 and 3")   # quicklz.go:94-96
-    if level == 1:
-        raise NotImplementedError("QuickLZ level-1 encoding is outside this build (DESIGN.md §7)")
     s = _as_bytes(source)
     if len(s) == 0:
         return None   # quicklz.go:109-111
     dst = ctypes.create_string_buffer(len(s) + 400)
-    n = _lib.lib().qlzx_compress1(s, dst, len(s), _lib.F_GO_COMPAT)
+    flags = _lib.F_LEVEL1 if level == 1 else _lib.F_GO_COMPAT
+    n = _lib.lib().qlzx_compress1(s, dst, len(s), flags)
     if n == 0:
         raise _lib.QlzxError("qlzx_compress1 failed: " + _lib.lib().qlzx_last_error().decode())
     return dst.raw[:n]
 
 
 def Decompress(source) -> bytes:
-    """quicklz.go:291-431.  Level 3 streams (level 1 raises, as Go panics for
-    levels other than 1/3 and this build decodes level 3 only)."""
+    """quicklz.go:291-431.  Compressed level-3 streams take the level-3 decoder
+    (K1/K2); stored streams of either level and compressed level-1 streams take
+    k_dec_go_l1 (Go's copy() semantics for a short stored body, zero-filled).
+    Where Go panics (level not 1/3, an index out of range on a corrupt stream)
+    this raises QuicklzError."""
     s = _as_bytes(source)
     level = (s[0] >> 2) & 3
     if level not in (1, 3):
         raise QuicklzError("Go version only supports level 1 and 3")
-    if level == 1:
-        raise NotImplementedError("QuickLZ level-1 decoding is outside this build (DESIGN.md §7)")
     n = SizeDecompressed(s)
     dst = ctypes.create_string_buffer(max(n, 1))
-    size = _lib.lib().qlz_decompress(s, dst, None)
+    if level == 3 and (s[0] & 1):
+        size = _lib.lib().qlz_decompress(s, dst, None)
+    else:
+        size = _lib.lib().qlzx_go_decompress1(s, len(s), dst, n)
     if size != n:
         raise QuicklzError(f"corrupt quicklz stream (status {_lib.lib().qlzx_last_error().decode()})")
     return dst.raw[:n]

@@ -119,9 +119,29 @@ int qlzx_compress_batch(const qlzx_blocks *b, uint32_t *csize, int32_t *status,
                         const uint32_t *crc_state, uint32_t *crc_out, uint32_t max_len,
                         uint32_t flags, void *workspace, size_t workspace_bytes, void *stream);
 
+#define QLZX_F_LEVEL1 2u    /* Go quicklz.Compress(src, 1) (quicklz.go:80-191): qlzx_compress1 only */
+
 /* Single-block helper on the GPU with `flags` (used by the quicklz.Compress mirror);
  * same contract as qlz_compress. */
 size_t qlzx_compress1(const void *source, char *destination, size_t size, uint32_t flags);
+
+/* ---- Go quicklz level 1 (quicklz.go:80-191 and 291-431) ----
+ * One lane per block with its hash tables in `workspace` (16-B aligned,
+ * qlzx_go_l1_workspace_size(n) bytes).  Production gobeansdb writes level 3 through
+ * cgo; these serve the Go Compress(src, 1) / Decompress surface.
+ * compress:   dst capacity >= src_len + 400 per block; empty block -> QLZX_E_EMPTY
+ *             (Go returns nil); output bytes = Go Compress(src, 1).
+ * decompress: Go Decompress of stored streams (any level) and compressed level-1
+ *             streams; QLZX_E_CORRUPT where Go would panic on an index, QLZX_E_LEVEL
+ *             for compressed level 3 (use qlzx_decompress_batch) and levels 0/2. */
+size_t qlzx_go_l1_workspace_size(uint32_t n);
+int qlzx_go_l1_compress_batch(const qlzx_blocks *b, uint32_t *csize, int32_t *status, void *workspace,
+                              size_t workspace_bytes, void *stream);
+int qlzx_go_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_t *dsize, int32_t *status,
+                             void *workspace, size_t workspace_bytes, void *stream);
+/* Single-block Go Decompress of a stored or level-1 stream of source_len bytes into
+ * destination (capacity dst_cap): returns the decompressed size, 0 on error. */
+size_t qlzx_go_decompress1(const char *source, size_t source_len, void *destination, size_t dst_cap);
 
 /* CRC32 of many buffers: out[i] = crc32_write(init ? init[i] : 0xffffffff, src_i) ^ (final_xor).
  * final_xor = 0 returns the raw state; 0xffffffff the store/crc32.go get() value. */

@@ -38,6 +38,10 @@ def lib():
         L.orc_compress_go.restype = sz
         L.orc_decompress.argtypes = [vp, sz, vp, sz, ctypes.POINTER(sz)]
         L.orc_decompress.restype = ctypes.c_int
+        L.orc_compress_go_l1.argtypes = [vp, sz, vp]
+        L.orc_compress_go_l1.restype = sz
+        L.orc_decompress_go_l1.argtypes = [vp, sz, vp, sz, ctypes.POINTER(sz)]
+        L.orc_decompress_go_l1.restype = ctypes.c_int
         L.orc_crc32_write.argtypes = [ctypes.c_uint32, vp, sz]
         L.orc_crc32_write.restype = ctypes.c_uint32
         L.orc_size_compressed.argtypes = [vp]
@@ -83,6 +87,27 @@ def decompress(data: bytes, cap: int | None = None):
     dst = np.zeros(max(cap, 1), dtype=np.uint8)
     out = ctypes.c_size_t(0)
     st = lib().orc_decompress(src.ctypes.data, len(data), dst.ctypes.data, cap, ctypes.byref(out))
+    return st, dst[: out.value].tobytes()
+
+
+def compress_go_l1(data: bytes) -> bytes | None:
+    """Go quicklz.Compress(data, 1) (quicklz.go:80-191); None for empty input (Go nil)."""
+    if not data:
+        return None
+    src = np.frombuffer(data, dtype=np.uint8)
+    dst = np.zeros(len(data) + 400, dtype=np.uint8)
+    r = lib().orc_compress_go_l1(src.ctypes.data, len(data), dst.ctypes.data)
+    return dst[:r].tobytes()
+
+
+def decompress_go_l1(data: bytes, cap: int | None = None):
+    """Go quicklz.Decompress of a level-1 or stored stream: (status, bytes)."""
+    src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    if cap is None:
+        cap = lib().orc_size_decompressed(src.ctypes.data) if len(data) >= 9 else 256
+    dst = np.zeros(max(cap, 1), dtype=np.uint8)
+    out = ctypes.c_size_t(0)
+    st = lib().orc_decompress_go_l1(src.ctypes.data, len(data), dst.ctypes.data, cap, ctypes.byref(out))
     return st, dst[: out.value].tobytes()
 
 
@@ -189,3 +214,47 @@ def ref_crc32_write(crc: int, data: bytes) -> int:
     _, C = ref()
     src = np.frombuffer(data, dtype=np.uint8)
     return C.crc32_write(crc, src.ctypes.data, len(data))
+
+
+_ref_l1 = None
+
+
+def ref_l1():
+    """The reference quicklz.c compiled at QuickLZ level 1 (oracle/_ref/libqlzref_l1.so,
+    container only); None when it is not built."""
+    global _ref_l1
+    if _ref_l1 is None:
+        q = os.path.join(HERE, "_ref", "libqlzref_l1.so")
+        if not os.path.exists(q):
+            build()
+        if not os.path.exists(q):
+            return None
+        Q = ctypes.CDLL(q)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        Q.qlz_compress.argtypes = [vp, vp, sz, vp]
+        Q.qlz_compress.restype = sz
+        Q.qlz_decompress.argtypes = [vp, vp, vp]
+        Q.qlz_decompress.restype = sz
+        Q.qlz_get_setting.argtypes = [ctypes.c_int]
+        Q.qlz_get_setting.restype = ctypes.c_int
+        _ref_l1 = Q
+    return _ref_l1
+
+
+def ref_l1_compress(data: bytes) -> bytes:
+    Q = ref_l1()
+    src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    dst = np.zeros(len(data) + 400, dtype=np.uint8)
+    scratch = np.zeros(max(Q.qlz_get_setting(1), 1) + 64, dtype=np.uint8)   # QLZ_SCRATCH_COMPRESS
+    r = Q.qlz_compress(src.ctypes.data, dst.ctypes.data, len(data), scratch.ctypes.data)
+    return dst[:r].tobytes()
+
+
+def ref_l1_decompress(data: bytes) -> bytes:
+    Q = ref_l1()
+    src = np.frombuffer(data, dtype=np.uint8)
+    n = lib().orc_size_decompressed(src.ctypes.data)
+    dst = np.zeros(n + 8, dtype=np.uint8)
+    scratch = np.zeros(max(Q.qlz_get_setting(2), 1) + 64, dtype=np.uint8)   # QLZ_SCRATCH_DECOMPRESS
+    r = Q.qlz_decompress(src.ctypes.data, dst.ctypes.data, scratch.ctypes.data)
+    return dst[:r].tobytes()

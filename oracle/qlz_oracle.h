@@ -43,6 +43,15 @@ size_t orc_compress(const uint8_t *src, size_t n, uint8_t *dst);
  * input returns 0 (nil).  dst must hold n + 400 bytes. */
 size_t orc_compress_go(const uint8_t *src, size_t n, uint8_t *dst);
 
+/* Go quicklz.Compress(src, 1) (quicklz.go:80-191,262-289; qlz_oracle_l1.c).  dst must hold
+ * n + 400 bytes.  Returns the compressed size, 0 (nil) for empty input. */
+size_t orc_compress_go_l1(const uint8_t *src, size_t n, uint8_t *dst);
+
+/* Go quicklz.Decompress (quicklz.go:291-431) of a stored stream (any level) or a compressed
+ * level-1 stream; ORC_E_CORRUPT where Go panics on an index, ORC_E_LEVEL for compressed
+ * level 3 (orc_decompress) and levels other than 1/3. */
+int orc_decompress_go_l1(const uint8_t *src, size_t src_len, uint8_t *dst, size_t dst_cap, size_t *out_len);
+
 /* Memory-safe level-3 decoder.  On valid streams the output equals
  * qlz_decompress (quicklz.c:777-836) and Go Decompress (quicklz.go:291-431).
  * Returns a status code; *out_len receives dsize on success. */
