@@ -15,8 +15,9 @@
 #include "qlzx_tables.hip"
 #include "qlzx_crc.hip"
 #include "qlzx_decode_wave.hip"
-#include "qlzx_decode_split.hip"
+#include "qlzx_decode_seq.hip"
 #include "qlzx_decode_lane8.hip"
+#include "qlzx_decode_split.hip"
 #include "qlzx_encode_lane.hip"
 #include "qlzx_encode_wg.hip"
 #include "qlzx_replay.hip"

@@ -109,7 +109,9 @@ __device__ int decode_lane8(const uint8_t *src, uint32_t len, uint8_t *dst, uint
 }
 
 // Handles blocks with dsize >= min_dsize (smaller ones belong to the fast path
-// when it runs; min_dsize = 0 -> all).
+// when it runs; min_dsize = 0 -> all).  min_dsize = kLane8Pending: only the fast-path-sized
+// blocks K1 left to this kernel (status kPending: a literal run too long for k_dec_seq).
+constexpr uint32_t kLane8Pending = 0xFFFFFFFFu;
 __global__ void __launch_bounds__(256) k_dec_lane8(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize,
                                                    int32_t *status, const uint32_t *crc_state,
                                                    const uint32_t *crc_expect, uint32_t *crc_out,
@@ -121,7 +123,11 @@ __global__ void __launch_bounds__(256) k_dec_lane8(qlzx_blocks b, const uint32_t
     if (i >= b.n) return;
     const uint8_t *src = b.src + b.src_off[i];
     const uint32_t len = b.src_len[i];
-    if (min_dsize && len >= 3) {
+    if (min_dsize == kLane8Pending) {
+        if (status[i] != kPending || len < 3) return;
+        const uint32_t hb = (src[0] & 2u) ? 9u : 3u;
+        if (len < hb || parse_header(src).dsize > QLZX_FAST_MAX_DSIZE) return;
+    } else if (min_dsize && len >= 3) {
         const uint32_t hb = (src[0] & 2u) ? 9u : 3u;
         if (len >= hb && parse_header(src).dsize < min_dsize) return;  // owned by the fast path
     }

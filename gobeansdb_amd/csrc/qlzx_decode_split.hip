@@ -509,7 +509,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     const uint32_t chunk = b.n < kChunkBlocks ? b.n : kChunkBlocks;
     const size_t o_rec = ((size_t)chunk * sizeof(BlkInfo) + 255) & ~(size_t)255;
     const size_t one = decode_wave_ws_bytes(b.n, max_dsize);
-    const size_t o_list = o_rec + ((((size_t)chunk * gmax * sizeof(GroupRec)) + 255) & ~(size_t)255);
+    const size_t o_list = o_rec + ((((size_t)chunk * rec_bytes_max(md)) + 255) & ~(size_t)255);
     const size_t o_aux = o_list + ((((size_t)b.n * sizeof(uint32_t)) + 255) & ~(size_t)255);
     static const bool sort_env = [] {  // QLZX_BLOCK_ORDER=0: chunk order (experiments)
         const char *e = getenv("QLZX_BLOCK_ORDER");
@@ -562,7 +562,9 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     // the split K2"); default: the item-per-lane kernel k_dec_blocks, which measured faster
     // (read per call so tests can run both kernels in one process)
     const char *k2e = getenv("QLZX_K2");
-    const bool k2_items = !(k2e && !strcmp(k2e, "split"));
+    const int k2mode = !k2e ? 0 : !strcmp(k2e, "split") ? 1 : !strcmp(k2e, "seq") ? 2 : 0;
+    const bool seq = k2mode == 2;
+    const uint32_t mcap = seq_mcap(md);
     const bool crc = crc_state || crc_expect || crc_out;
     if (overlap) (void)hipEventRecord(ev_k2[1], s), (void)hipStreamWaitEvent(side, ev_k2[1], 0);
     if (sort) {  // block order of the whole call, ahead of the first K1 (workspace half 0)
@@ -583,22 +585,28 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
         hipStream_t s1 = overlap ? side : s;
         if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
-        if (crc)
-            hipLaunchKernelGGL(k_dec_parse<true>, dim3((cnt + kParseWG<true> - 1) / kParseWG<true>),
-                               dim3(kParseWG<true>), 0, s1, b,
-                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order,
-                               max_dsize);
+        const dim3 g1c((cnt + kParseWG<true> - 1) / kParseWG<true>), g1((cnt + kParseWG<false> - 1) / kParseWG<false>);
+        if (crc && seq)
+            hipLaunchKernelGGL((k_dec_parse<true, true>), g1c, dim3(kParseWG<true>), 0, s1, b, dst_cap, dsize, status,
+                               crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order, max_dsize, mcap);
+        else if (seq)
+            hipLaunchKernelGGL((k_dec_parse<false, true>), g1, dim3(kParseWG<false>), 0, s1, b, dst_cap, dsize, status,
+                               crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order, max_dsize, mcap);
+        else if (crc)
+            hipLaunchKernelGGL((k_dec_parse<true>), g1c, dim3(kParseWG<true>), 0, s1, b, dst_cap, dsize, status,
+                               crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order, max_dsize, 0u);
         else
-            hipLaunchKernelGGL(k_dec_parse<false>, dim3((cnt + kParseWG<false> - 1) / kParseWG<false>),
-                               dim3(kParseWG<false>), 0, s1, b,
-                               dst_cap, dsize, status, crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order,
-                               max_dsize);
+            hipLaunchKernelGGL((k_dec_parse<false>), g1, dim3(kParseWG<false>), 0, s1, b, dst_cap, dsize, status,
+                               crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order, max_dsize, 0u);
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
 #ifndef QLZX_EXP_K2_EXTRA_LDS
 #define QLZX_EXP_K2_EXTRA_LDS 0  // experiments: extra dynamic LDS per WG to lower occupancy
 #endif
         // one kernel for every block size: the LDS window slides over longer blocks
-        if (k2_items)
+        if (seq)
+            hipLaunchKernelGGL(k_dec_seq<kWin>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
+                               (const uint32_t *)recs, mcap, (const uint32_t *)order);
+        else if (k2mode == 0)
             hipLaunchKernelGGL(k_dec_blocks<kWin>, dim3(cnt), dim3(64), QLZX_EXP_K2_EXTRA_LDS, s, b, dsize, status,
                                first, cnt, info, recs, gmax, (const uint32_t *)order);
         else
@@ -608,6 +616,9 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }
+    if (seq)  // blocks K1<SEQ> left to the general kernel (a literal run over kSeqRunMax items)
+        hipLaunchKernelGGL(k_dec_lane8, dim3((b.n + 255) / 256), dim3(256), 0, s, b, dst_cap, dsize, status,
+                           crc_state, crc_expect, crc_out, kLane8Pending);
     return 0;
 }
 

@@ -84,11 +84,19 @@ __host__ __device__ inline uint32_t groups_max(uint32_t max_dsize) { return max_
 
 inline bool decode_wave_enabled() { return true; }
 
+// per-block record area: group records (K2, split K2) or match records (k_dec_seq), in
+// whole GroupRecs so one stride (gmax_rec) serves both
+__host__ __device__ inline uint32_t rec_units_max(uint32_t md) {
+    const uint32_t seq_units = (4u * (md / 3u + 2u) + sizeof(GroupRec) - 1) / sizeof(GroupRec);
+    return groups_max(md) > seq_units ? groups_max(md) : seq_units;
+}
+inline size_t rec_bytes_max(uint32_t md) { return (size_t)rec_units_max(md) * sizeof(GroupRec); }
+
 inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
     const uint32_t md = max_dsize > QLZX_FAST_MAX_DSIZE ? QLZX_FAST_MAX_DSIZE : max_dsize;
     const uint32_t c = n < kChunkBlocks ? (n ? n : 1) : kChunkBlocks;
     return (((size_t)c * sizeof(BlkInfo) + 255) & ~(size_t)255) +
-           ((((size_t)c * groups_max(md) * sizeof(GroupRec)) + 255) & ~(size_t)255) +
+           ((((size_t)c * rec_bytes_max(md)) + 255) & ~(size_t)255) +
            ((((size_t)n * sizeof(uint32_t)) + 255) & ~(size_t)255) +              // block order, whole call
            1024 + 256;                                                            // order aux
 }
@@ -190,13 +198,24 @@ __device__ __forceinline__ void ring_issue(uint8_t *ring_wave, const uint8_t *gb
     }
 }
 
-template <bool CRC>
+// SEQ (K2 = k_dec_seq, qlzx_decode_seq.hip): instead of group records, one u32 per match,
+// I | X << 16 (I = item index, X = token bytes beyond the first of the matches before it, so
+// the token sits at hdr + 4 (I / 31 + 1) + I + X), `recs` read as u32[mcap] per block.  Such a
+// record needs I < 65536 and X < 65536, true of every valid stream of dsize <= 64 KiB (a match
+// emits >= 3 bytes, so #matches <= dsize / 3); the block is E_CORRUPT otherwise.  A literal run
+// of more than kSeqRunMax items leaves the block to the general path (kPending), so one K2
+// sequence (run + match) always fits half the output window.
+constexpr uint32_t kSeqRunMax = 1024;
+__host__ __device__ inline uint32_t seq_mcap(uint32_t max_dsize) { return max_dsize / 3u + 2u; }
+
+template <bool CRC, bool SEQ = false>
 __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, const uint32_t *dst_cap,
                                                          uint32_t *dsize_out, int32_t *status,
                                                          const uint32_t *crc_state, const uint32_t *crc_expect,
                                                          uint32_t *crc_out, uint32_t first, uint32_t count,
                                                          BlkInfo *info, GroupRec *recs, uint32_t gmax,
-                                                         const uint32_t *order, uint32_t max_dsize) {
+                                                         const uint32_t *order, uint32_t max_dsize,
+                                                         uint32_t mcap = 0) {
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG<CRC> / 64) * kRingWave];
     __shared__ uint32_t tab[CRC ? 8 * 256 : 1];
     if (CRC) {
@@ -248,6 +267,8 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
     // parse state
     uint32_t ip = hdr, g = 0, k = 31, cw = 0, m = 0, ra = 0, rb = 0, rec_ip = 0;
     GroupRec *myrec = recs + (size_t)(inrange ? lin : 0) * gmax;
+    uint32_t *mrec = (uint32_t *)recs + (size_t)(inrange ? lin : 0) * mcap;
+    uint32_t jm = 0, lit = 0;  // SEQ: match records written; literal items since the last match
     uint32_t crc = (CRC && inrange && crc_state) ? crc_state[i] : 0xffffffffu;
     bool done_parse = !parsing;
 
@@ -315,11 +336,27 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
                               (ip2 + 1 <= lim);
             const uint32_t ty2 = (w2 & 3u) + ((w2 & 127u) == 3u ? 1u : 0u);
             const uint32_t code2 = __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4);
-            const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) |  // C1, group bound
-                                         (mat & (ipm + code + 1 > csize)) |        // C2
-                                         (mat2 & (ip2 + code2 + 1 > csize)));
-            if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
-            st = bad ? QLZX_E_CORRUPT : st;
+            bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) |  // C1, group bound
+                                   (mat & (ipm + code + 1 > csize)) |        // C2
+                                   (mat2 & (ip2 + code2 + 1 > csize)));
+            bool pend = false;
+            if (SEQ) {
+                const uint32_t I1 = 31u * (g - 1u) + km, X1 = ipm - hdr - 4u * g - I1;
+                bad = bad | (stepping & mat & ((I1 >= dsize) | (X1 + (mat2 ? code : 0u) > 0xFFFFu) |
+                                               (jm + (mat2 ? 2u : 1u) > mcap)));
+                pend = stepping & !bad & mat & (lit + run > kSeqRunMax);
+                if (stepping & !bad & !pend & mat) {
+                    mrec[jm] = I1 | (X1 << 16);
+                    if (mat2) mrec[jm + 1] = (I1 + 1u) | ((X1 + code) << 16);
+                }
+            } else if (stepping & gb & (g > 0)) {
+                myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
+            }
+            if (SEQ) {
+                st = pend ? kPending : st;
+                bad = bad | pend;  // stops the parse like an error (the status stays kPending)
+            }
+            st = (bad & !pend) ? QLZX_E_CORRUPT : st;
             const bool adv = stepping & !bad;
             const bool ag = adv & gb;
             const uint32_t bm = mat ? (1u << (km & 31)) : 0u;
@@ -332,6 +369,10 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
             m = adv ? (gb ? 0u : m | bm | bm2) : m;
             ra = adv ? (gb ? 0u : ra | ((code & 1u) ? bm : 0u) | ((code2 & 1u) ? bm2 : 0u)) : ra;
             rb = adv ? (gb ? 0u : rb | ((code & 2u) ? bm : 0u) | ((code2 & 2u) ? bm2 : 0u)) : rb;
+            if (SEQ) {
+                jm += (adv & mat) ? (mat2 ? 2u : 1u) : 0u;
+                lit = (adv & !gb) ? (mat ? 0u : lit + run) : lit;
+            }
             done_parse = done_parse | (go & (end | bad));
             go = adv;
         }
@@ -341,11 +382,12 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
         ring_issue(ring, gbase, dummy, r + 3, last16, stream && r + 3 <= last_round);
     }
     PROF_MARK(4);  // 4: DMA issue + loop overhead
-    if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
+    if (!SEQ && parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
     PROF_FLUSH(0);
     vm_sync();
     if (!inrange) return;
     if (st == QLZX_OK && kind == kBlkCompressed && (!done_parse || g == 0)) st = QLZX_E_CORRUPT;
+    if (SEQ && st == QLZX_OK && kind == kBlkCompressed && lit > kSeqRunMax) st = kPending;  // trailing run
     if (CRC) {
         const uint32_t c = ~crc;
         if (crc_out) crc_out[i] = c;
@@ -359,6 +401,10 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
     } else if (kind == kBlkCompressed) {
         bi.ngroups = g;
         bi.nitems = (g - 1) * 31 + (k > 31 ? 31 : k);
+        if (SEQ) {  // ngroups -> match count; kind | (X after the last match) << 8 (<= 65535 + 3)
+            bi.ngroups = jm;
+            bi.kind = kind | ((ip - hdr - 4u * g - bi.nitems) << 8);
+        }
     }
     info[lin] = bi;
 }
@@ -610,8 +656,8 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
         uint32_t tokp;
         pm[kTokAhead - 1] = issue_tok<false>(gr4, cur, v4, nullptr, src, csize, &tokp);
         cur.next();
-        issue_rec(L.rec[rs8], rb, ((bt + kRecAhead) * 64) / 31, ngroups, lane);
         uint32_t *const bm = L.tok[ts];
+        GroupRec *const rslot8 = L.rec[rs8];
         ts = ts == kTokSlots - 1 ? 0 : ts + 1;
         rs4 = rs4 == kRecSlots - 1 ? 0 : rs4 + 1;
         rs8 = rs8 == kRecSlots - 1 ? 0 : rs8 + 1;
@@ -657,7 +703,9 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             const uint32_t s = d - off;
             const bool far = s < base;
             const bool spec = off < len || len > 16 || (far && (s + len > base || s < 3));  // byte / chunked path
-            uint32_t fy[5] = {0, 0, 0, 0, 0};
+            // only read under fc, which implies fload: no zero fill, whose register writes made
+            // the compiler wait (vmcnt) for every load still in flight, prefetch DMAs included
+            uint32_t fy[5];
 #ifdef QLZX_EXP_NOFAR  // experiment: far sources read garbage from LDS (timing only)
             const bool fload = false;
 #else
@@ -755,6 +803,10 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             if (__ballot(err)) { more = false; complete = false; }
         }
         if (__ballot(err)) break;
+        // the records of batch bt+kRecAhead, issued after this iteration's far loads were consumed:
+        // a DMA issued before them is in the in-order vmcnt queue ahead of them, so the far-load
+        // wait would also wait for it (c2: 41.0-41.4 -> 39.7-40.2 ms with the fy change above)
+        issue_rec(rslot8, rb, ((bt + kRecAhead) * 64) / 31, ngroups, lane);
         dma4(src + tokp, lds_addr(bm));  // tokens of batch bt+kTokAhead into the slot bt used (bitmap done)
         // DMAs of iterations <= bt - kK2Slack have landed
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QLZX_K2_VMWAIT) : "memory");

@@ -51,6 +51,9 @@ print("K1 parse iterations per wave-round: %.1f, active lanes per iteration (lan
 names2 = ["state reads", "prefetch issue", "decode+scan+checks", "sub-rounds", "wait prefetch", "write-out"]
 print("K2 per batch (cycles):", {nm: round(p[8 + j] / batches) for j, nm in enumerate(names2)})
 print("K2 per block total (cycles):", round(p[8:14].sum() / n))
+if True:
+    print("K2 seq per block (cycles):", {nm: round(p[8 + j] / n) for j, nm in enumerate(names2[:5])},
+          "sub-batches/block %.1f, sub-rounds/block %.1f" % (p[15] / n, p[14] / n))
 names3 = ["wait DMA", "item decode", "IP scan+checks+writes", "MP steps", "prefetch issue"]
 print("K2 split per IP batch (cycles):", {nm: round(p[16 + j] / batches) for j, nm in enumerate(names3)})
 print("K2 split per block total (cycles):", round(p[16:21].sum() / n))
