@@ -49,7 +49,8 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--blocks", type=int, default=1 << 20, help="blocks per GPU")
-    p.add_argument("--block-size", type=int, default=16384)
+    p.add_argument("--block-size", type=int, default=None,
+                   help="bytes per block (default: 16384; 65536 for --config c3 / --mode compress)")
     p.add_argument("--mode", choices=["decompress", "compress"], default="decompress")
     p.add_argument("--kind", choices=["text", "image"], default=None)
     p.add_argument("--unique", type=int, default=0,
@@ -60,7 +61,7 @@ def parse():
     p.add_argument("--crc", action="store_true", help="fused record CRC verify in the timed pass")
     p.add_argument("--traffic-json", default=None,
                    help="PMC HBM bytes per block (tools/traffic.py output); default: the committed "
-                        "profiles/r01_c2_traffic.json for the c2 workload")
+                        "profiles/r02_c2_traffic.json for the c2 workload")
     return p.parse_args()
 
 
@@ -97,6 +98,8 @@ def main():
         return bench_c5(args)
     if args.config == "c3":
         args.mode = "compress"
+    if args.block_size is None:  # BASELINE configs: c2 1 M x 16 KiB, c3 1 M x 64 KiB
+        args.block_size = 65536 if args.mode == "compress" else 16384
     from gobeansdb_amd import _lib, batch
 
     torch.cuda.set_device(local)
@@ -194,7 +197,7 @@ def main():
     achieved = (csum + dsum) / (kern_ms * 1e-3) / 1e9
     traffic = None
     if args.traffic_json is None and args.mode == "decompress" and kind == "text" and bs == 16384 and not args.crc:
-        args.traffic_json = os.path.join(ROOT, "profiles", "r01_c2_traffic.json")
+        args.traffic_json = os.path.join(ROOT, "profiles", "r02_c2_traffic.json")
     if args.traffic_json and os.path.exists(args.traffic_json):
         # PMC-measured HBM bytes per block (tools/traffic.py) x blocks per launch
         tj = json.load(open(args.traffic_json))
