@@ -126,6 +126,15 @@ constexpr uint32_t kParseRounds = 4;  // segment-walker rounds before the serial
 //             wave' = the wave owning the output index), accumulated while
 //             scattering so the next pass needs no count loop
 //   counted   cnt already holds this pass's counts (from the previous scatter)
+// Counter slot of logical counter L = key * W + wave: one padding word per key row, so the
+// lanes of one wave (same wave, different keys) hit different LDS banks.  Without it a
+// 16-wave workgroup's row stride of 16 words put all 64 lanes on 4 banks.
+template <uint32_t W>
+__device__ __forceinline__ uint32_t cslot(uint32_t L) {
+    return L + L / W;
+}
+constexpr uint32_t cslots(uint32_t nkeys, uint32_t W) { return nkeys * (W + 1); }
+
 template <uint32_t W, uint32_t NB_LOG2, typename OUT>
 __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t *in, OUT *out, uint32_t shift,
                                  uint32_t *cnt, uint64_t *wsum, unsigned long long *sub, uint32_t *hist,
@@ -153,7 +162,7 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
     constexpr uint32_t U = 4;  // 64-element batches per iteration: their list loads are in flight together
     SUB_MARK(0);
     if (!counted) {
-        for (uint32_t k = tid; k < NC; k += T) cnt[k] = 0;
+        for (uint32_t k = tid; k < cslots(NB, W); k += T) cnt[k] = 0;
         __syncthreads();
         for (uint32_t base = r0; base < r1; base += 64 * U) {
             uint32_t pv[U];
@@ -166,7 +175,7 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
             for (uint32_t u = 0; u < U; u++) {
                 if (base + 64 * u + lane < r1) {
                     const uint32_t h = hash12(fetch24(s_in, pv[u]));
-                    atomicAdd(&cnt[((h >> shift) & (NB - 1)) * W + wave], 1u);
+                    atomicAdd(&cnt[cslot<W>(((h >> shift) & (NB - 1)) * W + wave)], 1u);
                     if (hist) atomicAdd(&hist[h >> 1], 1u << (16 * (h & 1u)));
                 }
             }
@@ -180,7 +189,7 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
         uint32_t sum = 0;
 #pragma unroll
         for (uint32_t j = 0; j < CPT; j++) {
-            v[j] = own ? cnt[CPT * tid + j] : 0u;
+            v[j] = own ? cnt[cslot<W>(CPT * tid + j)] : 0u;
             sum += v[j];
         }
         uint64_t tot;
@@ -188,7 +197,7 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
         if (own) {
 #pragma unroll
             for (uint32_t j = 0; j < CPT; j++) {
-                cnt[CPT * tid + j] = ex;
+                cnt[cslot<W>(CPT * tid + j)] = ex;
                 ex += v[j];
             }
         }
@@ -213,12 +222,12 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
         const uint64_t peers = match_peers<NB_LOG2>(key, __ballot(valid));
         const uint32_t intra = __popcll(peers & ltm);
         uint32_t cur = 0;
-        if (valid) cur = cnt[key * W + wave];
+        if (valid) cur = cnt[cslot<W>(key * W + wave)];
         // every lane's read is issued before the leader's write (in-order LDS per wave)
-        if (valid && intra == 0) cnt[key * W + wave] = cur + (uint32_t)__popcll(peers);
+        if (valid && intra == 0) cnt[cslot<W>(key * W + wave)] = cur + (uint32_t)__popcll(peers);
         if (valid) {
             out[cur + intra] = (OUT)(sizeof(OUT) == 2 ? p : p | ((f >> 12) << 16));
-            if (next_cnt) atomicAdd(&next_cnt[(h >> 4) * W + __umulhi(cur + intra, per_magic)], 1u);
+            if (next_cnt) atomicAdd(&next_cnt[cslot<W>((h >> 4) * W + __umulhi(cur + intra, per_magic))], 1u);
         }
       }
     }
@@ -230,16 +239,16 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
 // passes: low 4 hash bits, then the bucket group), as gl[t] = pos | fetch[23:12] << 16,
 // plus bst[h] = the sorted index where bucket h starts (exclusive scan of the
 // bucket histogram counted in the first pass).  tmp: u16[P] scratch; s_hist:
-// 2048 words of LDS free during the sort; s_cnt: 272 * W words.
+// 2048 words of LDS free during the sort; s_cnt: 272 * (W + 1) words.
 template <uint32_t W>
 __device__ void bucket_sort(const uint8_t *s_in, uint32_t P, uint16_t *tmp, uint32_t *gl, uint16_t *bst,
                             uint32_t *s_cnt, uint32_t *s_hist, uint64_t *wsum, unsigned long long *subA,
                             unsigned long long *subB) {
     constexpr uint32_t T = 64 * W;
     const uint32_t tid = threadIdx.x;
-    uint32_t *cntB = s_cnt, *cntA = s_cnt + kEncGroups * W;
+    uint32_t *cntB = s_cnt, *cntA = s_cnt + cslots(kEncGroups, W);
     for (uint32_t k = tid; k < QLZX_BUCKETS / 2; k += T) s_hist[k] = 0;
-    for (uint32_t k = tid; k < kEncGroups * W; k += T) cntB[k] = 0;
+    for (uint32_t k = tid; k < cslots(kEncGroups, W); k += T) cntB[k] = 0;
     // (pass A zeroes its own counters and syncs before counting)
     stable_partition<W, 4>(s_in, P, nullptr, tmp, 0, cntA, wsum, subA, s_hist, cntB, false);
     // bucket starts: exclusive scan of the u16-pair histogram, bucket order = sorted order
@@ -278,7 +287,7 @@ struct WgCfg {
     static constexpr uint32_t U_B = IN_B + L8_B;                          // s_in | s_l8
     static constexpr uint32_t BM_LOG2 = CAP >= 65536 ? 20 : (CAP >= 16384 ? 18 : 16);  // proof bitmap bits
     static constexpr uint32_t NCW = (CAP + 30) / 31;
-    static constexpr uint32_t SC1 = (kEncGroups + 16) * W;  // phase 1 counters (both radix passes)
+    static constexpr uint32_t SC1 = cslots(kEncGroups + 16, W);  // phase 1 counters (both radix passes)
     static constexpr uint32_t SC4 = 2 * NCW;         // phase 4 control words + positions
     static constexpr uint32_t SC3 = (T + 2) + 2 * T;  // phase 3 exits + serial-walk segment bits
     static constexpr uint32_t SCR = SC1 > SC4 ? (SC1 > SC3 ? SC1 : SC3) : (SC4 > SC3 ? SC4 : SC3);
