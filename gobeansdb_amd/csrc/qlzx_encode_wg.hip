@@ -355,8 +355,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             for (uint32_t k = tid * 4; k < BMW; k += T * 4) *(uint4 *)(bm + k) = make_uint4(0, 0, 0, 0);
             __syncthreads();
             const uint32_t ny = n - 2;  // positions holding a whole 3-gram
-            for (uint32_t y0 = tid * 16; y0 < ny; y0 += T * 16) {
-                uint32_t w[5];
+            auto load20 = [&](uint32_t y0, uint32_t w[5]) {
                 if (y0 + 20 <= n) {
                     const uint4 v = *(const uint4 *)(src + y0);
                     w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
@@ -372,6 +371,8 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                         w[j] = x;
                     }
                 }
+            };
+            auto mark16 = [&](uint32_t y0, const uint32_t w[5]) {
 #pragma unroll 4
                 for (uint32_t j = 0; j < 16; j++) {
                     if (y0 + j < ny) {
@@ -381,6 +382,15 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                         atomicOr(&bm[h >> 5], bit);  // no return: D = ny - distinct hashes
                     }
                 }
+            };
+            // two 16-position steps per iteration, both loads in flight before either is hashed
+            for (uint32_t y0 = tid * 16; y0 < ny; y0 += 2 * T * 16) {
+                uint32_t wa[5], wb[5] = {0, 0, 0, 0, 0};
+                const uint32_t y1 = y0 + T * 16;
+                load20(y0, wa);
+                if (y1 < ny) load20(y1, wb);
+                mark16(y0, wa);
+                if (y1 < ny) mark16(y1, wb);
             }
             __syncthreads();
             uint32_t ones = 0;
@@ -393,7 +403,26 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             __syncthreads();
             stored = stored_proof(n, ny - s_misc[1]);
             if (stored) {  // quicklz.c:722-727 from the global copy of the input
-                if ((((uintptr_t)dst) & 3u) == 0) {
+                if ((((uintptr_t)dst) & 15u) == 0) {
+                    // 16 B per thread per step, four steps' loads in flight before any store
+                    // (one dependent load per step made the copy latency-bound: 70 K cycles)
+                    const uint32_t tot = n + hdr, a0 = (hdr + 15u) & ~15u, a1 = tot & ~15u;
+                    constexpr uint32_t K = 4;
+                    for (uint32_t o0 = a0 + tid * 16; o0 < a1; o0 += T * 16 * K) {
+                        uint4 v[K];
+#pragma unroll
+                        for (uint32_t k = 0; k < K; k++) {
+                            const uint32_t o = min(o0 + k * T * 16, a1 - 16);  // clamped: loads unconditional
+                            const uint32_t *q = (const uint32_t *)(src + o - hdr);  // unaligned loads
+                            v[k] = make_uint4(q[0], q[1], q[2], q[3]);
+                        }
+#pragma unroll
+                        for (uint32_t k = 0; k < K; k++)
+                            if (o0 + k * T * 16 < a1) *(uint4 *)(dst + o0 + k * T * 16) = v[k];
+                    }
+                    for (uint32_t o = hdr + tid; o < tot; o += T)
+                        if (o < a0 || o >= a1) dst[o] = src[o - hdr];
+                } else if ((((uintptr_t)dst) & 3u) == 0) {
                     const uint32_t tot = n + hdr, a0 = (hdr + 3u) & ~3u;
                     for (uint32_t o = a0 + tid * 4; o + 4 <= tot; o += T * 4)
                         *(uint32_t *)(dst + o) = *(const uint32_t *)(src + o - hdr);  // unaligned load
