@@ -66,7 +66,7 @@ constexpr uint32_t kRingWave = kRingSlots * kRoundBytes * 64;  // 16 KiB per wav
 #endif
 constexpr uint32_t kWin = QLZX_K2_WIN;          // K2 LDS history window (bytes)
 #ifndef QLZX_K2_SLACK
-#define QLZX_K2_SLACK 3
+#define QLZX_K2_SLACK 1  // round 2: 1 beats 3 (c2 39.1 vs 39.9 ms, c5 482.6 vs 455 GiB/s)
 #endif
 constexpr uint32_t kK2Slack = QLZX_K2_SLACK;  // K2: iterations a prefetch DMA has to land
 constexpr uint32_t kTokAhead = kK2Slack + 1;   // tokens of batch bt + kTokAhead issued in iteration bt
@@ -438,8 +438,10 @@ struct K2Lds {
 // "s_waitcnt vmcnt(2 * kK2Slack)" at the end of iteration bt means "everything
 // issued up to iteration bt - kK2Slack has landed".  Iteration bt issues the
 // tokens of bt + kTokAhead and the records of bt + kRecAhead, so both have
-// kK2Slack whole iterations to arrive.  Slack 2 saves 320 B of LDS per wave
-// (29 -> 31 waves/CU) but measured within noise of slack 3 (c2 and c5), so 3 stays.
+// kK2Slack whole iterations to arrive.  Slack 1 (the default since round 2) keeps 640 B less
+// LDS and two fewer in-flight batch registers per wave than slack 3 and measured faster on
+// c2 (39.1 vs 39.9 ms, interleaved runs) and c5 (482.6 vs 455 GiB/s): the wave issues about
+// a whole iteration of work between a DMA and its use, which covers the DMA at this occupancy.
 template <bool DMA = true>
 __device__ __forceinline__ void issue_rec(GroupRec *slot, const GroupRec *rb, uint32_t g0, uint32_t ngroups,
                                           uint32_t lane) {
