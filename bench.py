@@ -370,7 +370,8 @@ def bench_compress(args, rank, world, dev, kind):
         doff = dst.off[:ns].cpu().numpy()
         csh = cs[:ns].cpu().numpy()
         gpu_comp = [dh[int(doff[j]): int(doff[j]) + int(csh[j])].tobytes() for j in range(ns)]
-        cpu = cpu_baseline(kind, bs, args.cpu_seconds, mode="compress", gpu_comp=gpu_comp)
+        gpu_crc = crc[:ns].cpu().numpy().view(np.uint32).tolist()
+        cpu = cpu_baseline(kind, bs, args.cpu_seconds, mode="compress", gpu_comp=gpu_comp, gpu_crc=gpu_crc)
     if rank == 0:
         rec = {
             "metric": "GiB/s device-resident QuickLZ decompress (+compress), batched 4-64 KiB values",
@@ -420,7 +421,7 @@ def host_cpus() -> tuple[int, int, str]:
     return usable, os.cpu_count() or usable, model
 
 
-def cpu_baseline(kind: str, bs: int, seconds: float, mode: str = "decompress", gpu_comp=None):
+def cpu_baseline(kind: str, bs: int, seconds: float, mode: str = "decompress", gpu_comp=None, gpu_crc=None):
     """The reference codec (oracle/_ref) -- else the C restatement -- on the host cores over a
     bounded sample of the same workload: every usable core (the process's affinity mask;
     nproc reported beside it), one core, and the cgo-faithful form that allocates the
@@ -428,7 +429,8 @@ def cpu_baseline(kind: str, bs: int, seconds: float, mode: str = "decompress", g
 
     gpu_comp: the GPU encoder's bytes for blocks 0.. of the same generator; each must equal
     the CPU codec's output for that block (sampled bit-exactness of the
-    compressed bytes), else the bench fails."""
+    compressed bytes), else the bench fails.  gpu_crc: the fused CRC32 of those blocks (c3),
+    checked against zlib.crc32 of the CPU codec's bytes (= store/crc32.go)."""
     from oracle import oracle as O
     threads, nproc, model = host_cpus()
     L = O.lib()
@@ -476,6 +478,12 @@ def cpu_baseline(kind: str, bs: int, seconds: float, mode: str = "decompress", g
             if g != want:
                 raise SystemExit(f"GPU-compressed block {j} differs from the CPU codec's bytes")
         parity = f"{len(gpu_comp)} GPU-compressed blocks == oracle/qlz_oracle.c bytes (pinned to quicklz.c)"
+        if gpu_crc is not None:
+            import zlib
+            for j, c in enumerate(gpu_crc):
+                if int(c) != zlib.crc32(gpu_comp[j]):
+                    raise SystemExit(f"fused CRC of block {j} != zlib.crc32 of its bytes")
+            parity += f"; their fused CRC32 == zlib.crc32 (store/crc32.go)"
     gibs, reps = run(threads, seconds, False)
     if not comp_mode and Q is not None and not all(
             dst[int(o): int(o) + bs].tobytes() == p_ for o, p_ in zip(off_d[:8], plain[:8])):
