@@ -561,9 +561,8 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     // QLZX_K2=split: the item-phase/match-phase kernel (k_dec_split, DESIGN.md §4 "Round 2:
     // the split K2"); default: the item-per-lane kernel k_dec_blocks, which measured faster
     // (read per call so tests can run both kernels in one process)
-    const char *k2e = getenv("QLZX_K2");
-    const int k2mode = !k2e ? 0 : !strcmp(k2e, "split") ? 1 : !strcmp(k2e, "seq") ? 2 : 0;
-    const bool seq = k2mode == 2;
+    const int k2mode = (int)k2_mode();
+    const bool seq = k2mode == kK2Seq;
     const uint32_t mcap = seq_mcap(md);
     const bool crc = crc_state || crc_expect || crc_out;
     if (overlap) (void)hipEventRecord(ev_k2[1], s), (void)hipStreamWaitEvent(side, ev_k2[1], 0);

@@ -84,13 +84,21 @@ __host__ __device__ inline uint32_t groups_max(uint32_t max_dsize) { return max_
 
 inline bool decode_wave_enabled() { return true; }
 
-// per-block record area: group records (K2, split K2) or match records (k_dec_seq), in
-// whole GroupRecs so one stride (gmax_rec) serves both
-__host__ __device__ inline uint32_t rec_units_max(uint32_t md) {
-    const uint32_t seq_units = (4u * (md / 3u + 2u) + sizeof(GroupRec) - 1) / sizeof(GroupRec);
-    return groups_max(md) > seq_units ? groups_max(md) : seq_units;
+// K2 kernel of this process: QLZX_K2 = (unset) | split | seq; read per call, so tests can
+// run every kernel in one process.  Only seq changes the workspace (match records).
+enum K2Mode { kK2Items = 0, kK2Split = 1, kK2Seq = 2 };
+inline K2Mode k2_mode() {
+    const char *e = getenv("QLZX_K2");
+    return !e ? kK2Items : !strcmp(e, "split") ? kK2Split : !strcmp(e, "seq") ? kK2Seq : kK2Items;
 }
-inline size_t rec_bytes_max(uint32_t md) { return (size_t)rec_units_max(md) * sizeof(GroupRec); }
+
+// per-block record area in whole GroupRecs: group records (K2, split K2), or with
+// QLZX_K2=seq the match records of k_dec_seq (u32 per match, up to dsize/3 + 2: 2.6x more)
+inline size_t rec_bytes_max(uint32_t md) {
+    const uint32_t seq_units = (4u * (md / 3u + 2u) + sizeof(GroupRec) - 1) / sizeof(GroupRec);
+    const uint32_t units = k2_mode() == kK2Seq && seq_units > groups_max(md) ? seq_units : groups_max(md);
+    return (size_t)units * sizeof(GroupRec);
+}
 
 inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
     const uint32_t md = max_dsize > QLZX_FAST_MAX_DSIZE ? QLZX_FAST_MAX_DSIZE : max_dsize;
