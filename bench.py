@@ -204,7 +204,7 @@ def main():
         traffic = round(tj["hbm_bytes_per_block"] * n)
 
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N = 1 only
         # the first 256 GPU-compressed blocks of rank 0 = blocks 0..255 of the CPU leg's sample
         ns = min(256, uniq)
         cb = cbuf[: int(coff[ns - 1]) + int(cs_all[ns - 1])].cpu().numpy()
@@ -364,7 +364,7 @@ def bench_compress(args, rank, world, dev, kind):
     if os.path.exists(tj) and kind == "image" and bs == 65536:
         traffic = round(json.load(open(tj))["hbm_bytes_per_block"] * n)
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N = 1 only
         ns = min(256, n)
         dh = dst.data[: int(dst.off[ns - 1]) + bs + 400].cpu().numpy()
         doff = dst.off[:ns].cpu().numpy()
