@@ -88,6 +88,8 @@ __device__ __forceinline__ SeqRec seq_rec(uint32_t rw, uint32_t jj, uint32_t nma
     return r;
 }
 
+constexpr uint32_t kSeqWin = 4096;  // k_dec_seq's own window (independent of QLZX_K2_WIN)
+
 template <uint32_t W>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLZX_SQ_WAVES_PER_EU)))
 k_dec_seq(qlzx_blocks b, uint32_t *dsize_out, int32_t *status, uint32_t first, uint32_t count,

@@ -603,7 +603,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
 #endif
         // one kernel for every block size: the LDS window slides over longer blocks
         if (seq)
-            hipLaunchKernelGGL(k_dec_seq<kWin>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
+            hipLaunchKernelGGL(k_dec_seq<kSeqWin>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
                                (const uint32_t *)recs, mcap, (const uint32_t *)order);
         else if (k2mode == 0)
             hipLaunchKernelGGL(k_dec_blocks<kWin>, dim3(cnt), dim3(64), QLZX_EXP_K2_EXTRA_LDS, s, b, dsize, status,

@@ -813,6 +813,20 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             if (__ballot(err)) { more = false; complete = false; }
         }
         if (__ballot(err)) break;
+#ifdef QLZX_EXP_PADV  // experiment: extra dependent VALU per batch (issue-bound test; timing only)
+        {
+            uint32_t x = lane;
+            for (int j = 0; j < QLZX_EXP_PADV; j++) asm volatile("v_add_u32 %0, %0, 1" : "+v"(x));
+            asm volatile("" ::"v"(x));
+        }
+#endif
+#ifdef QLZX_EXP_PADS  // experiment: extra dependent SALU per batch
+        {
+            uint32_t x = bt;
+            for (int j = 0; j < QLZX_EXP_PADS; j++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(x)::"scc");
+            asm volatile("" ::"s"(x));
+        }
+#endif
         // the records of batch bt+kRecAhead, issued after this iteration's far loads were consumed:
         // a DMA issued before them is in the in-order vmcnt queue ahead of them, so the far-load
         // wait would also wait for it (c2: 41.0-41.4 -> 39.7-40.2 ms with the fy change above)
