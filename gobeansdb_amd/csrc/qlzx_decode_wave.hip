@@ -546,6 +546,67 @@ struct Copy16 {
     }
 };
 
+// Match sub-rounds when every pending match takes the plain 16-B copy (no byte or chunked
+// path): per sub-round, ready = pending & no pending lane in `need`, copied under exec = ready.
+// The compiled form of this loop spent ~37 of its ~55 instructions per sub-round on turning
+// per-lane bools into masks and back; here the pending set stays in two SGPRs and the
+// readiness test is three VALU.  The lowest pending lane's `need` holds only lanes below it
+// (need lies inside [owner(s), owner(send - 1)], send <= d), so every sub-round copies at least
+// that lane and the loop ends.  LDS operations of a wave execute in issue order, so a
+// sub-round's reads observe the previous sub-round's ds_mskor writes.
+__device__ __forceinline__ void subrounds_plain(uint64_t pend, uint64_t need, const Copy16 &cp, uint8_t *win) {
+    uint32_t plo = (uint32_t)pend, phi = (uint32_t)(pend >> 32);
+    const uint32_t nlo = (uint32_t)need, nhi = (uint32_t)(need >> 32);
+    const uint32_t xaddr = (uint32_t)(uintptr_t)(win + cp.xa), qaddr = (uint32_t)(uintptr_t)(win + cp.qa);
+    uint64_t sv;
+    uint32_t st, t, x0, x1, x2, x3, x4, x5;
+    asm volatile(
+        "s_mov_b64 %[sv], exec\n"
+        "1:\n"
+        "v_and_b32 %[t], %[plo], %[nlo]\n"
+        "v_and_or_b32 %[t], %[phi], %[nhi], %[t]\n"
+        "v_cmp_eq_u32 vcc, 0, %[t]\n"
+        "s_and_b32 vcc_lo, vcc_lo, %[plo]\n"
+        "s_and_b32 vcc_hi, vcc_hi, %[phi]\n"
+        "s_andn2_b32 %[plo], %[plo], vcc_lo\n"
+        "s_andn2_b32 %[phi], %[phi], vcc_hi\n"
+        "s_mov_b64 exec, vcc\n"
+        "ds_read_b32 %[x0], %[xa]\n"
+        "ds_read_b32 %[x1], %[xa] offset:4\n"
+        "ds_read_b32 %[x2], %[xa] offset:8\n"
+        "ds_read_b32 %[x3], %[xa] offset:12\n"
+        "ds_read_b32 %[x4], %[xa] offset:16\n"
+        "ds_read_b32 %[x5], %[xa] offset:20\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_alignbyte_b32 %[t], %[x1], %[x0], %[sh]\n"
+        "v_and_b32 %[t], %[t], %[m0]\n"
+        "ds_mskor_b32 %[qa], %[m0], %[t]\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_alignbyte_b32 %[x0], %[x2], %[x1], %[sh]\n"
+        "v_and_b32 %[x0], %[x0], %[m1]\n"
+        "ds_mskor_b32 %[qa], %[m1], %[x0] offset:4\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_alignbyte_b32 %[x1], %[x3], %[x2], %[sh]\n"
+        "v_and_b32 %[x1], %[x1], %[m2]\n"
+        "ds_mskor_b32 %[qa], %[m2], %[x1] offset:8\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_alignbyte_b32 %[x2], %[x4], %[x3], %[sh]\n"
+        "v_and_b32 %[x2], %[x2], %[m3]\n"
+        "ds_mskor_b32 %[qa], %[m3], %[x2] offset:12\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_alignbyte_b32 %[x3], %[x5], %[x4], %[sh]\n"
+        "v_and_b32 %[x3], %[x3], %[m4]\n"
+        "ds_mskor_b32 %[qa], %[m4], %[x3] offset:16\n"
+        "s_mov_b64 exec, %[sv]\n"
+        "s_or_b32 %[st], %[plo], %[phi]\n"
+        "s_cbranch_scc1 1b\n"
+        : [sv] "=&s"(sv), [plo] "+s"(plo), [phi] "+s"(phi), [st] "=&s"(st), [t] "=&v"(t), [x0] "=&v"(x0),
+          [x1] "=&v"(x1), [x2] "=&v"(x2), [x3] "=&v"(x3), [x4] "=&v"(x4), [x5] "=&v"(x5)
+        : [nlo] "v"(nlo), [nhi] "v"(nhi), [xa] "v"(xaddr), [qa] "v"(qaddr), [sh] "v"(cp.sh), [m0] "v"(cp.mk[0]),
+          [m1] "v"(cp.mk[1]), [m2] "v"(cp.mk[2]), [m3] "v"(cp.mk[3]), [m4] "v"(cp.mk[4])
+        : "vcc", "scc", "memory");
+}
+
 // Inclusive prefix sum over the 64 lanes with DPP (row shifts + row broadcasts).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
@@ -582,6 +643,41 @@ __device__ __forceinline__ void far_load20(const uint8_t *dst, uint32_t a0, uint
         a = a + 4 <= lim ? a : lim - 4;
         y[j] = *(const uint32_t *)(dst + a);  // unaligned dword load (unaligned access mode)
     }
+}
+
+// K2's far loads when a0 + 20 <= the block's dsize (the caller checks base + 20 <= dsize: a far
+// source lies below base), so no per-dword clamp: five unaligned dword loads (unaligned access
+// mode).
+// QLZX_K2_FARFAST=1: unclamped far loads (fewer VALU, but 66 VGPRs -> 7 waves/SIMD: c2 38.0 ->
+// 39.2 ms); off by default
+#ifndef QLZX_K2_FARFAST
+#define QLZX_K2_FARFAST 0
+#endif
+#ifndef QLZX_K2_FAR_W
+#define QLZX_K2_FAR_W 1
+#endif
+__device__ __forceinline__ void far_load20_fast(const uint8_t *dst, uint32_t a0, uint32_t y[5]) {
+#if QLZX_K2_FAR_W == 8
+    const uint8_t *p = dst + a0;
+    const uint2 u = *(const uint2 *)p, v = *(const uint2 *)(p + 8);
+    y[0] = u.x, y[1] = u.y, y[2] = v.x, y[3] = v.y;
+    y[4] = *(const uint32_t *)(p + 16);
+#elif QLZX_K2_FAR_W == 16
+    const uint8_t *p = dst + a0;
+    const uint4 u = *(const uint4 *)p;
+    y[0] = u.x, y[1] = u.y, y[2] = u.z, y[3] = u.w;
+    y[4] = *(const uint32_t *)(p + 16);
+#elif QLZX_K2_FAR_W == 4
+    const uint32_t *q = (const uint32_t *)(dst + a0);
+    y[0] = q[0], y[1] = q[1], y[2] = q[2], y[3] = q[3], y[4] = q[4];
+#else  // five dword loads from opaque offsets: merged loads need aligned register tuples (66 VGPRs)
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        uint32_t a = a0 + 4 * j;
+        asm volatile("" : "+v"(a));
+        y[j] = *(const uint32_t *)(dst + a);
+    }
+#endif
 }
 
 #ifndef QLZX_K2_WAVES_PER_EU
@@ -722,7 +818,13 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             const bool fload = in && valid && ism && far && !spec;
 #endif
             if (__ballot(fload)) {
-                if (fload) far_load20(dst, s - (d & 3u), dsize, fy);
+                // a far source ends below base: its 20-B read stays inside the block unless the
+                // window base is within 20 B of the end (wave-uniform; then the clamped loads)
+                if (QLZX_K2_FARFAST && base + 20 <= dsize) {
+                    if (fload) far_load20_fast(dst, s - (d & 3u), fy);
+                } else {
+                    if (fload) far_load20(dst, s - (d & 3u), dsize, fy);
+                }
             }
             // ---- checks C2-C5 on the live items (those that start before dsize) ----
             const bool live = in && valid && d < dsize;
@@ -777,6 +879,12 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             }
             uint64_t pend = __ballot(!done);
             const bool spec_any = __ballot(!done && spec) != 0;  // rare: skip its test per sub-round
+#ifndef QLZX_K2_CLOOP
+            if (!spec_any) {  // every pending match takes the 16-B copy: the hand-scheduled loop
+                if (pend) subrounds_plain(pend, need, cp, win);
+                pend = 0;
+            }
+#endif
             while (pend) {
                 // exact: every byte of the source is final once none of the lanes owning it is pending
                 const bool ready = !done & ((need & pend) == 0);
