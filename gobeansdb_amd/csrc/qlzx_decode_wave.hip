@@ -648,10 +648,12 @@ __device__ __forceinline__ void far_load20(const uint8_t *dst, uint32_t a0, uint
 // K2's far loads when a0 + 20 <= the block's dsize (the caller checks base + 20 <= dsize: a far
 // source lies below base), so no per-dword clamp: five unaligned dword loads (unaligned access
 // mode).
-// QLZX_K2_FARFAST=1: unclamped far loads (fewer VALU, but 66 VGPRs -> 7 waves/SIMD: c2 38.0 ->
-// 39.2 ms); off by default
+// QLZX_K2_FARFAST=1 (default): far loads without the per-dword clamp; while the window base is
+// within 20 B of the block's end, far lanes take the byte path instead (c2 38.09 -> 37.79 ms).
+// Merged 16-B far loads (FAR_W=16) measured the same; a per-lane clamp/fast branch needed 66
+// VGPRs (7 waves/SIMD) and lost.
 #ifndef QLZX_K2_FARFAST
-#define QLZX_K2_FARFAST 0
+#define QLZX_K2_FARFAST 1
 #endif
 #ifndef QLZX_K2_FAR_W
 #define QLZX_K2_FAR_W 1
@@ -808,7 +810,10 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             // far sources (below the window, already in HBM): load them first, use them in the first sub-round
             const uint32_t s = d - off;
             const bool far = s < base;
-            const bool spec = off < len || len > 16 || (far && (s + len > base || s < 3));  // byte / chunked path
+            // byte / chunked path; with FARFAST also every far source while the window base is within 20 B
+            // of the block's end (wave-uniform, rare), so far_load20_fast never reads past dsize
+            const bool nearend = QLZX_K2_FARFAST && base + 20 > dsize;
+            const bool spec = off < len || len > 16 || (far && (s + len > base || s < 3 || nearend));
             // only read under fc, which implies fload: no zero fill, whose register writes made
             // the compiler wait (vmcnt) for every load still in flight, prefetch DMAs included
             uint32_t fy[5];
@@ -819,12 +824,12 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
 #endif
             if (__ballot(fload)) {
                 // a far source ends below base: its 20-B read stays inside the block unless the
-                // window base is within 20 B of the end (wave-uniform; then the clamped loads)
-                if (QLZX_K2_FARFAST && base + 20 <= dsize) {
-                    if (fload) far_load20_fast(dst, s - (d & 3u), fy);
-                } else {
-                    if (fload) far_load20(dst, s - (d & 3u), dsize, fy);
-                }
+                // window base is within 20 B of the end (FARFAST: then those lanes are spec)
+#if QLZX_K2_FARFAST
+                if (fload) far_load20_fast(dst, s - (d & 3u), fy);
+#else
+                if (fload) far_load20(dst, s - (d & 3u), dsize, fy);
+#endif
             }
             // ---- checks C2-C5 on the live items (those that start before dsize) ----
             const bool live = in && valid && d < dsize;
