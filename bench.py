@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--crc", action="store_true", help="fused record CRC verify in the timed pass")
     p.add_argument("--traffic-json", default=None,
                    help="PMC HBM bytes per block (tools/traffic.py output); default: the committed "
-                        "profiles/r02_c2_traffic.json for the c2 workload")
+                        "profiles/r02b_c2_traffic.json for the c2 workload")
     return p.parse_args()
 
 
@@ -197,7 +197,7 @@ def main():
     achieved = (csum + dsum) / (kern_ms * 1e-3) / 1e9
     traffic = None
     if args.traffic_json is None and args.mode == "decompress" and kind == "text" and bs == 16384 and not args.crc:
-        args.traffic_json = os.path.join(ROOT, "profiles", "r02_c2_traffic.json")
+        args.traffic_json = os.path.join(ROOT, "profiles", "r02b_c2_traffic.json")
     if args.traffic_json and os.path.exists(args.traffic_json):
         # PMC-measured HBM bytes per block (tools/traffic.py) x blocks per launch
         tj = json.load(open(args.traffic_json))
