@@ -10,7 +10,10 @@ Multi-GPU: one process per GPU (torch.distributed.run); each rank owns an
 independent shard of blocks (weak scaling, no data-path collective); timing is
 barrier + synchronize bracketed and max-reduced over ranks.
 
-Prints one JSON line (rank 0).  See DESIGN.md §6 for the roofline accounting.
+Prints one JSON line (rank 0).  See DESIGN.md §3 for the roofline accounting.  The default c2
+run (1 M x 16 KiB) also measures BASELINE config c3 -- compress + fused CRC32 of 1 M x 64 KiB
+image-like values, the "(+compress)" of the metric -- after releasing the c2 buffers, and reports
+it under "compress" in the same line (--no-c3 skips it; --config c3 runs it alone).
 """
 from __future__ import annotations
 
@@ -58,6 +61,9 @@ def parse():
     p.add_argument("--gen-chunk", type=int, default=1 << 16)
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-c3", action="store_true",
+                   help="c2 run: skip the c3 compress leg reported under \"compress\" in the same line")
+    p.add_argument("--c3-steps", type=int, default=3, help="timed steps of the c3 compress leg")
     p.add_argument("--crc", action="store_true", help="fused record CRC verify in the timed pass")
     p.add_argument("--traffic-json", default=None,
                    help="PMC HBM bytes per block (tools/traffic.py output); default: the committed "
@@ -235,6 +241,21 @@ def main():
                          "algorithmic_bytes_per_launch": csum + dsum},
             "cpu_baseline": cpu,
         }
+    comp = None
+    if not args.no_c3 and args.mode == "decompress" and args.block_size == 16384 and args.blocks == 1 << 20:
+        # BASELINE config c3 (the "+compress" of the metric) in the same driver run: the c2 buffers
+        # are released first; value/roofline/cpu_baseline of c3 go under "compress"
+        del src, out, cbuf, ws, coff_t, src_off, src_len
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        a3 = argparse.Namespace(**vars(args))
+        a3.mode, a3.block_size, a3.steps, a3.warmup = "compress", 65536, args.c3_steps, 1
+        a3.traffic_json = None
+        comp = bench_compress(a3, rank, world, dev, "image", emit=False)
+    if rank == 0:
+        if comp is not None:
+            rec["compress"] = {k: comp[k] for k in ("value", "unit", "steps", "warmup", "ms_per_step", "config",
+                                                    "roofline", "cpu_baseline")}
         print(json.dumps(rec), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
@@ -283,7 +304,7 @@ def bench_c5(args):
     return bench_c5.main()
 
 
-def bench_compress(args, rank, world, dev, kind):
+def bench_compress(args, rank, world, dev, kind, emit: bool = True):
     """Config c3: compress every block of the rank's shard (1 M x 64 KiB image-like by default) with
     the fused record CRC, inputs resident in HBM.  Verified before timing by a device round trip
     (compress -> decompress == input) and a CRC recomputation over the outputs."""
@@ -388,9 +409,11 @@ def bench_compress(args, rank, world, dev, kind):
                          "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": n * bs + csum},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(rec), flush=True)
-    if world > 1:
+        if emit:
+            print(json.dumps(rec), flush=True)
+    if world > 1 and emit:
         torch.distributed.destroy_process_group()
+    return rec if rank == 0 else None
 
 
 REF_WHAT = ("reference quicklz/quicklz.c {fn} (oracle/_ref/libqlzref.so, gcc -O2 as cgo builds it)")
