@@ -847,6 +847,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             PROF_MARK(2);  // 2: decode + scan + checks
             // literals (non-literal lanes store to an unused byte past the window)
             win[(live && !ism) ? d - base : W + 24] = (uint8_t)t;
+            PROF_MARK(0);  // 0: literal stores
             // ---- matches: which in-sub-batch lanes each match's source needs ----
             // Bit r of the bitmap bm marks an item starting at D + r.  The lane owning
             // byte D + r is sub0 + (#starts at or before r) - 1; a match needs the lanes owning
@@ -873,6 +874,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             const uint32_t n16 = len < 16 ? len : 16;
             Copy16 cp;
             cp.prep(d - base, off, n16);
+            PROF_MARK(6);  // 6: bitmap, owner lookups, need mask, copy masks
             // far matches (source in HBM, below the window) depend on no lane of this batch:
             // copy them before the sub-rounds, so the loop needs no source select
             {
@@ -882,6 +884,7 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                 }
                 done = done || fc;
             }
+            PROF_MARK(7);  // 7: far copies (waits for the far loads)
             uint64_t pend = __ballot(!done);
             const bool spec_any = __ballot(!done && spec) != 0;  // rare: skip its test per sub-round
 #ifndef QLZX_K2_CLOOP

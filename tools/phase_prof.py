@@ -48,9 +48,10 @@ names1 = ["pre-loop", "wait DMA", "CRC", "parse", "issue+end"]
 print("K1 per wave per round (cycles):", {nm: round(p[j] / waves_k1 / rounds) for j, nm in enumerate(names1)})
 print("K1 parse iterations per wave-round: %.1f, active lanes per iteration (lane 0 only sampled): %.2f"
       % (p[5] / waves_k1 / rounds, p[6] / max(p[5], 1)))
-names2 = ["state reads", "prefetch issue", "decode+scan+checks", "sub-rounds", "wait prefetch", "write-out"]
+names2 = ["literal stores", "prefetch issue", "decode+scan+checks", "sub-rounds", "wait prefetch", "write-out",
+          "bitmap+owner+masks", "far copies"]
 print("K2 per batch (cycles):", {nm: round(p[8 + j] / batches) for j, nm in enumerate(names2)})
-print("K2 per block total (cycles):", round(p[8:14].sum() / n))
+print("K2 per block total (cycles):", round(p[8:16].sum() / n))
 if True:
     print("K2 seq per block (cycles):", {nm: round(p[8 + j] / n) for j, nm in enumerate(names2[:5])},
           "sub-batches/block %.1f, sub-rounds/block %.1f" % (p[15] / n, p[14] / n))
