@@ -381,7 +381,7 @@ def bench_compress(args, rank, world, dev, kind, emit: bool = True):
     value = tot["in_bytes"] * args.steps / wall / 2**30
     achieved = (n * bs + csum) / (kern_ms * 1e-3) / 1e9
     traffic = None
-    tj = args.traffic_json or os.path.join(ROOT, "profiles", "r01_c3_traffic.json")
+    tj = args.traffic_json or os.path.join(ROOT, "profiles", "r02b_c3_traffic.json")
     if os.path.exists(tj) and kind == "image" and bs == 65536:
         traffic = round(json.load(open(tj))["hbm_bytes_per_block"] * n)
     cpu = None

@@ -1,6 +1,8 @@
 """HBM traffic per block of the decode kernels from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
 
-usage: python tools/traffic.py gpurun_out/TAG NBLOCKS OUT.json
+usage: python tools/traffic.py gpurun_out/TAG NBLOCKS OUT.json [KERNEL_SUBSTRINGS]
+KERNEL_SUBSTRINGS: comma-separated kernel-name filters (default "k_dec_parse,k_dec_blocks";
+"k_encode_wg" for the c3 encoder).
 FETCH_SIZE/WRITE_SIZE are KiB per dispatch.  Per MI355X_MICROARCH.md (HBM section)
 FETCH_SIZE counts half the bytes of 16-B-per-lane streaming reads on gfx950, so it
 is doubled; WRITE_SIZE is exact for 16-B-per-lane stores (K2's write-out).
@@ -13,14 +15,16 @@ import sys
 from collections import defaultdict
 
 root, nblocks, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
+pats = sys.argv[4].split(",") if len(sys.argv) > 4 else ["k_dec_parse", "k_dec_blocks"]
 per = defaultdict(lambda: defaultdict(float))  # (kernel, dispatch) -> counter -> value
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     with open(f) as fh:
         for r in csv.DictReader(fh):
             name = r.get("Kernel_Name", "")
-            if "k_dec_" not in name:
+            hit = [q for q in pats if q in name]
+            if not hit:
                 continue
-            k = "k_dec_parse" if "k_dec_parse" in name else "k_dec_blocks"
+            k = hit[0]
             per[(k, f, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
 tot = defaultdict(lambda: defaultdict(list))
 for (k, f, d), c in per.items():
