@@ -13,7 +13,9 @@ barrier + synchronize bracketed and max-reduced over ranks.
 Prints one JSON line (rank 0).  See DESIGN.md §3 for the roofline accounting.  The default c2
 run (1 M x 16 KiB) also measures BASELINE config c3 -- compress + fused CRC32 of 1 M x 64 KiB
 image-like values, the "(+compress)" of the metric -- after releasing the c2 buffers, and reports
-it under "compress" in the same line (--no-c3 skips it; --config c3 runs it alone).
+it under "compress" in the same line (--no-c3 skips it; --config c3 runs it alone); then config c5
+-- 400 GiB of mixed 4-64 KiB values split over the ranks, strong scaling -- under "mixed"
+(--no-c5 skips it; --config c5 runs it alone).
 """
 from __future__ import annotations
 
@@ -64,6 +66,9 @@ def parse():
     p.add_argument("--no-c3", action="store_true",
                    help="c2 run: skip the c3 compress leg reported under \"compress\" in the same line")
     p.add_argument("--c3-steps", type=int, default=3, help="timed steps of the c3 compress leg")
+    p.add_argument("--no-c5", action="store_true",
+                   help="c2 run: skip the c5 leg (400 GiB of mixed values over the ranks, strong "
+                        "scaling) reported under \"mixed\" in the same line")
     p.add_argument("--crc", action="store_true", help="fused record CRC verify in the timed pass")
     p.add_argument("--traffic-json", default=None,
                    help="PMC HBM bytes per block (tools/traffic.py output); default: the committed "
@@ -252,10 +257,23 @@ def main():
         a3.mode, a3.block_size, a3.steps, a3.warmup = "compress", 65536, args.c3_steps, 1
         a3.traffic_json = None
         comp = bench_compress(a3, rank, world, dev, "image", emit=False)
+    mixed = None
+    if not args.no_c5 and args.mode == "decompress" and args.block_size == 16384 and args.blocks == 1 << 20:
+        # BASELINE config c5 in the same run: 400 GiB of mixed 4-64 KiB values split over the
+        # ranks (strong scaling), so the driver's 1/2/4/8-GPU runs also measure it
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_c5
+        mixed = bench_c5.run(argparse.Namespace(total_gib=400.0, round_gib=16.0, warmup=1, gen_chunk=1 << 15),
+                             rank, world, dev)
     if rank == 0:
         if comp is not None:
             rec["compress"] = {k: comp[k] for k in ("value", "unit", "steps", "warmup", "ms_per_step", "config",
                                                     "roofline", "cpu_baseline")}
+        if mixed is not None:
+            rec["mixed"] = {k: mixed[k] for k in ("metric", "value", "unit", "scaling", "rounds_per_gpu", "wall_s",
+                                                  "config", "roofline")}
         print(json.dumps(rec), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

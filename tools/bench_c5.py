@@ -4,7 +4,8 @@
 BASELINE.json configs[4] / SURVEY §8(d) c5.  The job is a fixed total of decompressed
 output (--total-gib, 400 by default) split evenly over the ranks.  400 GiB does not fit
 one GPU, so each rank keeps ONE device-resident round of --round-gib GiB of output
-(compressed inputs + output buffer in HBM) and decompresses it ceil(share / round) times.
+(compressed inputs + output buffer in HBM, share / rounds bytes with rounds = ceil(share /
+round-gib)) and decompresses it `rounds` times, so the job totals --total-gib at every N.
 Every round replays the same resident blocks: refilling a round from host memory is the
 PCIe leg that config c4 (tools/bench_replay.py) measures, not part of this number.
 
@@ -47,7 +48,7 @@ def main():
     p.add_argument("--gen-chunk", type=int, default=1 << 15)
     args = p.parse_args()
 
-    from gobeansdb_amd import _lib, batch, shard
+    from gobeansdb_amd import shard
 
     rank, world, local = shard.env_rank()
     torch.cuda.set_device(local)
@@ -55,11 +56,26 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
+    rec = run(args, rank, world, dev)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def run(args, rank, world, dev):
+    """The c5 job on this rank (process group, if any, already initialised); returns the
+    record on rank 0, None elsewhere.  args: total_gib, round_gib, warmup, gen_chunk."""
+    from gobeansdb_amd import _lib, batch, shard
+
     log(f"{world} rank(s); lib: {_lib.info()}")
 
     # ---- this rank's resident round: mixed sizes and kinds, seeded per rank ----
     rng = np.random.default_rng([SEED, rank])
-    target = int(args.round_gib * 2**30)
+    # the rank's share in whole rounds of at most round_gib: the job totals total_gib at every N
+    share = args.total_gib * 2**30 / world
+    rounds = max(1, math.ceil(share / (args.round_gib * 2**30)))
+    target = int(share / rounds)
     sizes = []
     tot = 0
     while tot < target:
@@ -113,8 +129,6 @@ def main():
     log("device round trip verified (per-block CRC32)")
 
     # ---- timed: this rank's share of the job, in rounds over the resident set ----
-    share = args.total_gib * 2**30 / world
-    rounds = max(1, math.ceil(share / dsum))
     stream = torch.cuda.current_stream()
 
     def one_round():
@@ -161,9 +175,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4)},
         }
-        print(json.dumps(rec), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+        return rec
+    return None
 
 
 if __name__ == "__main__":
