@@ -264,8 +264,8 @@ def main():
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         sys.path.insert(0, os.path.join(ROOT, "tools"))
-        import bench_c5
-        mixed = bench_c5.run(argparse.Namespace(total_gib=400.0, round_gib=16.0, warmup=1, gen_chunk=1 << 15),
+        import bench_c5 as c5mod
+        mixed = c5mod.run(argparse.Namespace(total_gib=400.0, round_gib=16.0, warmup=1, gen_chunk=1 << 15),
                              rank, world, dev)
     if rank == 0:
         if comp is not None:

@@ -33,3 +33,20 @@ def test_world_mismatch_refused():
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_main_does_not_shadow_module_functions():
+    """bench.main() dispatches to module-level functions (bench_c5, bench_compress, ...); a local
+    import of the same name inside main() would make those calls fail at run time."""
+    import ast
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    tree = ast.parse(src)
+    top = {f.name for f in tree.body if isinstance(f, ast.FunctionDef)}
+    main = next(f for f in tree.body if isinstance(f, ast.FunctionDef) and f.name == "main")
+    local = set()
+    for n in ast.walk(main):
+        if isinstance(n, (ast.Import, ast.ImportFrom)):
+            local |= {(a.asname or a.name).split(".")[0] for a in n.names}
+        elif isinstance(n, ast.Name) and isinstance(n.ctx, ast.Store):
+            local.add(n.id)
+    assert not (local & top), f"main() shadows module functions: {sorted(local & top)}"
