@@ -373,13 +373,23 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 }
             };
             auto mark16 = [&](uint32_t y0, const uint32_t w[5]) {
-#pragma unroll 4
-                for (uint32_t j = 0; j < 16; j++) {
-                    if (y0 + j < ny) {
+                // fully unrolled (w[] indices static: a partial unroll turned every w[j / 4] into a
+                // select chain); the per-position range test only in the block's last piece
+                if (y0 + 16 <= ny) {
+#pragma unroll
+                    for (uint32_t j = 0; j < 16; j++) {
                         const uint32_t f = __builtin_amdgcn_alignbyte(w[j / 4 + 1], w[j / 4], j & 3) & 0xFFFFFFu;
                         const uint32_t h = (f * 0x9E3779B1u) >> (32 - C::BM_LOG2);
-                        const uint32_t bit = 1u << (h & 31u);
-                        atomicOr(&bm[h >> 5], bit);  // no return: D = ny - distinct hashes
+                        atomicOr(&bm[h >> 5], 1u << (h & 31u));  // no return: D = ny - distinct hashes
+                    }
+                } else {
+#pragma unroll
+                    for (uint32_t j = 0; j < 16; j++) {
+                        if (y0 + j < ny) {
+                            const uint32_t f = __builtin_amdgcn_alignbyte(w[j / 4 + 1], w[j / 4], j & 3) & 0xFFFFFFu;
+                            const uint32_t h = (f * 0x9E3779B1u) >> (32 - C::BM_LOG2);
+                            atomicOr(&bm[h >> 5], 1u << (h & 31u));
+                        }
                     }
                 }
             };
