@@ -53,7 +53,10 @@ constexpr uint32_t kBlkSkip = 0, kBlkStored = 1, kBlkCompressed = 2;
 // four waves share one 8 KiB slicing-by-8 table (8 waves/CU instead of 6)
 template <bool CRC>
 constexpr uint32_t kParseWG = CRC ? 256 : 64;
-constexpr uint32_t kChunkBlocks = 131072;  // >= 256 CUs x 8 waves x 64 lanes: K1 fills the chip
+#ifndef QLZX_CHUNK_BLOCKS
+#define QLZX_CHUNK_BLOCKS 131072
+#endif
+constexpr uint32_t kChunkBlocks = QLZX_CHUNK_BLOCKS;  // >= 256 CUs x 8 waves x 64 lanes: K1 fills the chip
 #ifndef QLZX_K1_ROUND
 #define QLZX_K1_ROUND 64
 #endif
