@@ -50,3 +50,14 @@ def test_main_does_not_shadow_module_functions():
         elif isinstance(n, ast.Name) and isinstance(n.ctx, ast.Store):
             local.add(n.id)
     assert not (local & top), f"main() shadows module functions: {sorted(local & top)}"
+
+
+def test_c5_rounds_total_400_gib_at_every_n():
+    """bench's c5 leg (tools/bench_c5.py) is strong scaling: the job is 400 GiB at N = 1..8."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_c5
+    for world in (1, 2, 4, 8):
+        rounds, target = bench_c5.plan_rounds(400.0, 16.0, world)
+        assert target <= 16 * 2**30
+        assert abs(rounds * target * world - 400 * 2**30) <= world * rounds
+    assert bench_c5.plan_rounds(400.0, 16.0, 1) == (25, 16 * 2**30)

@@ -63,6 +63,14 @@ def main():
         torch.distributed.destroy_process_group()
 
 
+def plan_rounds(total_gib: float, round_gib: float, world: int) -> tuple[int, int]:
+    """(rounds, resident bytes per rank): the rank's share of the job in whole rounds of at most
+    round_gib, so rounds x resident x world = total_gib at every N (to a block)."""
+    share = total_gib * 2**30 / world
+    rounds = max(1, math.ceil(share / (round_gib * 2**30)))
+    return rounds, int(share / rounds)
+
+
 def run(args, rank, world, dev):
     """The c5 job on this rank (process group, if any, already initialised); returns the
     record on rank 0, None elsewhere.  args: total_gib, round_gib, warmup, gen_chunk."""
@@ -72,10 +80,7 @@ def run(args, rank, world, dev):
 
     # ---- this rank's resident round: mixed sizes and kinds, seeded per rank ----
     rng = np.random.default_rng([SEED, rank])
-    # the rank's share in whole rounds of at most round_gib: the job totals total_gib at every N
-    share = args.total_gib * 2**30 / world
-    rounds = max(1, math.ceil(share / (args.round_gib * 2**30)))
-    target = int(share / rounds)
+    rounds, target = plan_rounds(args.total_gib, args.round_gib, world)
     sizes = []
     tot = 0
     while tot < target:
