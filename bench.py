@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--no-c3", action="store_true",
                    help="c2 run: skip the c3 compress leg reported under \"compress\" in the same line")
     p.add_argument("--c3-steps", type=int, default=3, help="timed steps of the c3 compress leg")
+    p.add_argument("--legs-small", action="store_true",
+                   help="rehearsal only: run the c3 and c5 legs at this run's --blocks and a 1 GiB c5 job")
     p.add_argument("--no-c5", action="store_true",
                    help="c2 run: skip the c5 leg (400 GiB of mixed values over the ranks, strong "
                         "scaling) reported under \"mixed\" in the same line")
@@ -113,11 +115,18 @@ def main():
         args.block_size = 65536 if args.mode == "compress" else 16384
     from gobeansdb_amd import _lib, batch
 
+    # one GPU per rank; on a box with fewer GPUs than ranks (a rehearsal, QLZX_BENCH_PG=gloo)
+    # ranks share devices round-robin
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("QLZX_BENCH_PG", "nccl")  # nccl = RCCL; gloo only to rehearse N > 1
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     kind = args.kind or ("text" if args.mode == "decompress" else "image")
     if args.mode == "compress":
         return bench_compress(args, rank, world, dev, kind)
@@ -247,7 +256,8 @@ def main():
             "cpu_baseline": cpu,
         }
     comp = None
-    if not args.no_c3 and args.mode == "decompress" and args.block_size == 16384 and args.blocks == 1 << 20:
+    legs = args.mode == "decompress" and args.block_size == 16384 and (args.blocks == 1 << 20 or args.legs_small)
+    if not args.no_c3 and legs:
         # BASELINE config c3 (the "+compress" of the metric) in the same driver run: the c2 buffers
         # are released first; value/roofline/cpu_baseline of c3 go under "compress"
         del src, out, cbuf, ws, coff_t, src_off, src_len
@@ -258,14 +268,15 @@ def main():
         a3.traffic_json = None
         comp = bench_compress(a3, rank, world, dev, "image", emit=False)
     mixed = None
-    if not args.no_c5 and args.mode == "decompress" and args.block_size == 16384 and args.blocks == 1 << 20:
+    if not args.no_c5 and legs:
         # BASELINE config c5 in the same run: 400 GiB of mixed 4-64 KiB values split over the
         # ranks (strong scaling), so the driver's 1/2/4/8-GPU runs also measure it
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import bench_c5 as c5mod
-        mixed = c5mod.run(argparse.Namespace(total_gib=400.0, round_gib=16.0, warmup=1, gen_chunk=1 << 15),
+        tg, rg = (1.0, 0.25) if args.legs_small else (400.0, 16.0)
+        mixed = c5mod.run(argparse.Namespace(total_gib=tg, round_gib=rg, warmup=1, gen_chunk=1 << 15),
                              rank, world, dev)
     if rank == 0:
         if comp is not None:
