@@ -233,6 +233,9 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
         for (uint32_t t = threadIdx.x; t < 8 * 256; t += kParseWG<CRC>) tab[t] = g_crc_slice8[t];
         __syncthreads();
     }
+#if QLZX_K1_PRIO > 0
+    __builtin_amdgcn_s_setprio(QLZX_K1_PRIO);  // experiments: K1 waves above K2's in issue arbitration
+#endif
     const uint32_t lane = threadIdx.x & 63;
     uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWave;
     const uint32_t lin = blockIdx.x * kParseWG<CRC> + threadIdx.x;
@@ -655,6 +658,12 @@ __device__ __forceinline__ void far_load20(const uint8_t *dst, uint32_t a0, uint
 // within 20 B of the block's end, far lanes take the byte path instead (c2 38.09 -> 37.79 ms).
 // Merged 16-B far loads (FAR_W=16) measured the same; a per-lane clamp/fast branch needed 66
 // VGPRs (7 waves/SIMD) and lost.
+#ifndef QLZX_K1_PRIO
+#define QLZX_K1_PRIO 0
+#endif
+#ifndef QLZX_K2_PRIO
+#define QLZX_K2_PRIO 0
+#endif
 #ifndef QLZX_K2_FARFAST
 #define QLZX_K2_FARFAST 1
 #endif
@@ -698,6 +707,11 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
     const uint32_t lane = threadIdx.x;
     const uint32_t bx = blockIdx.x;  // workspace slot
     if (bx >= count) return;
+#if QLZX_K2_PRIO > 0
+    // K2 waves above K1's (priority 0) in the SIMD's issue arbitration: K1 of the next chunk,
+    // which has the whole K2 to hide under, takes the slots K2 leaves idle
+    __builtin_amdgcn_s_setprio(QLZX_K2_PRIO);
+#endif
     const uint32_t i = list ? list[bx] : first + bx;  // block
     const BlkInfo bi = info[bx];
     if (bi.kind == kBlkSkip) return;
