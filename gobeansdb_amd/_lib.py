@@ -24,6 +24,7 @@ STATUS_NAMES = ["OK", "E_SIZE_COMPRESSED", "E_CORRUPT", "E_LEVEL", "E_DST_CAP", 
 
 F_GO_COMPAT = 1
 F_LEVEL1 = 2
+GO_ERROR = (1 << (8 * ctypes.sizeof(ctypes.c_size_t))) - 1   # QLZX_GO_ERROR, (size_t)-1
 
 
 class QlzxError(RuntimeError):
@@ -43,6 +44,7 @@ def header_functions() -> list[str]:
     """Every function declared in include/qlzx.h."""
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"^\s*#.*$", "", text, flags=re.M)   # preprocessor lines (#define X (...))
     return sorted(set(re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", text)))
 
 
@@ -79,6 +81,8 @@ def lib() -> ctypes.CDLL:
     L.qlzx_compress1.restype = sz
     L.qlzx_go_l1_workspace_size.argtypes = [u32]
     L.qlzx_go_l1_workspace_size.restype = sz
+    L.qlzx_go_decompress_workspace_size.argtypes = [u32]
+    L.qlzx_go_decompress_workspace_size.restype = sz
     L.qlzx_go_l1_compress_batch.argtypes = [BP, vp, vp, vp, sz, vp]
     L.qlzx_go_l1_compress_batch.restype = ctypes.c_int
     L.qlzx_go_decompress_batch.argtypes = [BP, vp, vp, vp, vp, sz, vp]
@@ -99,6 +103,8 @@ def lib() -> ctypes.CDLL:
     L.qlzx_replay_index.restype = ctypes.c_int
     L.qlzx_vhash_batch.argtypes = [vp, vp, vp, u32, vp, vp]
     L.qlzx_vhash_batch.restype = ctypes.c_int
+    L.qlzx_last_status.argtypes = []
+    L.qlzx_last_status.restype = ctypes.c_int
     L.qlzx_last_error.argtypes = []
     L.qlzx_last_error.restype = ctypes.c_char_p
     L.qlzx_info.argtypes = [ctypes.c_char_p, sz]

@@ -176,7 +176,7 @@ def go_decompress(src: BlockBatch, dst: BlockBatch, *, dst_cap: torch.Tensor | N
     dev = src.data.device
     dsize = torch.zeros(n, dtype=torch.int32, device=dev)
     status = torch.full((n,), -1, dtype=torch.int32, device=dev)
-    ws_bytes = L.qlzx_go_l1_workspace_size(n)
+    ws_bytes = L.qlzx_go_decompress_workspace_size(n)
     ws = (workspace or Workspace(dev)).get(ws_bytes)
     b = _blocks(src, dst.data, dst.off)
     rc = L.qlzx_go_decompress_batch(ctypes.byref(b), _ptr(dst_cap), dsize.data_ptr(), status.data_ptr(),

@@ -15,9 +15,7 @@
 #include "qlzx_tables.hip"
 #include "qlzx_crc.hip"
 #include "qlzx_decode_wave.hip"
-#include "qlzx_decode_seq.hip"
 #include "qlzx_decode_lane8.hip"
-#include "qlzx_decode_split.hip"
 #include "qlzx_encode_lane.hip"
 #include "qlzx_encode_wg.hip"
 #include "qlzx_replay.hip"
@@ -117,13 +115,8 @@ int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_
     if (!b->src || !b->src_off || !b->src_len || !b->dst || !b->dst_off)
         return fail(QLZX_R_BAD_ARG, "qlzx_decompress_batch: null block array");
     hipStream_t s = (hipStream_t)stream;
-    static const bool lane8 = [] {
-        const char *e = getenv("QLZX_DECODE");
-        return e && !strcmp(e, "lane8");
-    }();
-    // QLZX_DECODE=lane8 (experiments) or no workspace: the general lane-per-block kernel for every block
-    const bool fast = !lane8 && qlzx::decode_wave_enabled() && workspace &&
-                      workspace_bytes >= qlzx::decode_wave_ws_bytes(b->n, max_dsize);
+    // no workspace: the general lane-per-block kernel for every block
+    const bool fast = workspace && workspace_bytes >= qlzx::decode_wave_ws_bytes(b->n, max_dsize);
     if (fast) {
         int r = qlzx::launch_decode_wave(*b, dst_cap, dsize, status, crc_state, crc_expect, crc_out,
                                          max_dsize, workspace, workspace_bytes, s);
@@ -132,7 +125,7 @@ int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_
     if (!fast || max_dsize > QLZX_FAST_MAX_DSIZE) {
         const uint32_t min_dsize = fast ? QLZX_FAST_MAX_DSIZE + 1 : 0;
         hipLaunchKernelGGL(qlzx::k_dec_lane8, dim3((b->n + 255) / 256), dim3(256), 0, s, *b, dst_cap,
-                           dsize, status, crc_state, crc_expect, crc_out, min_dsize);
+                           dsize, status, crc_state, crc_expect, crc_out, min_dsize, max_dsize);
         HIP_OK(hipGetLastError());
     }
     return QLZX_R_OK;
@@ -173,35 +166,48 @@ int qlzx_compress_batch(const qlzx_blocks *b, uint32_t *csize, int32_t *status,
     return QLZX_R_OK;
 }
 
-size_t qlzx_go_l1_workspace_size(uint32_t n) { return (size_t)n * qlzx::kL1WsBlock; }
+size_t qlzx_go_l1_workspace_size(uint32_t n) {
+    return (size_t)std::min<uint32_t>(std::max<uint32_t>(n, 1), qlzx::kL1Chunk) * qlzx::kL1WsBlock;
+}
+size_t qlzx_go_decompress_workspace_size(uint32_t n) {
+    return (size_t)std::min<uint32_t>(std::max<uint32_t>(n, 1), qlzx::kL1Chunk) * qlzx::kL1DecWsBlock;
+}
 
 static int check_l1_args(const qlzx_blocks *b, const void *out, void *workspace, size_t workspace_bytes,
-                         const char *who) {
+                         size_t need, const char *who) {
     if (!b || !out) return fail(QLZX_R_BAD_ARG, who);
     if (b->n == 0) return QLZX_R_OK;
     if (!b->src || !b->src_off || !b->src_len || !b->dst || !b->dst_off) return fail(QLZX_R_BAD_ARG, who);
-    if (!workspace || (((uintptr_t)workspace) & 15u) || workspace_bytes < qlzx_go_l1_workspace_size(b->n))
-        return fail(QLZX_R_WORKSPACE, who);
+    if (!workspace || (((uintptr_t)workspace) & 15u) || workspace_bytes < need) return fail(QLZX_R_WORKSPACE, who);
     return QLZX_R_OK;
 }
 
 int qlzx_go_l1_compress_batch(const qlzx_blocks *b, uint32_t *csize, int32_t *status, void *workspace,
                               size_t workspace_bytes, void *stream) {
-    if (int r = check_l1_args(b, csize, workspace, workspace_bytes, "qlzx_go_l1_compress_batch")) return r;
-    if (b->n == 0) return QLZX_R_OK;
-    hipLaunchKernelGGL(qlzx::k_enc_go_l1, dim3((b->n + 63) / 64), dim3(64), 0, (hipStream_t)stream, *b, csize,
-                       status, (uint8_t *)workspace);
-    HIP_OK(hipGetLastError());
+    if (int r = check_l1_args(b, csize, workspace, workspace_bytes, qlzx_go_l1_workspace_size(b ? b->n : 0),
+                              "qlzx_go_l1_compress_batch"))
+        return r;
+    // chunks of kL1Chunk blocks reuse the workspace (same stream: in order)
+    for (uint32_t first = 0; first < b->n; first += qlzx::kL1Chunk) {
+        const uint32_t cnt = std::min<uint32_t>(b->n - first, qlzx::kL1Chunk);
+        hipLaunchKernelGGL(qlzx::k_enc_go_l1, dim3((cnt + 63) / 64), dim3(64), 0, (hipStream_t)stream, *b, csize,
+                           status, (uint8_t *)workspace, first, cnt);
+        HIP_OK(hipGetLastError());
+    }
     return QLZX_R_OK;
 }
 
 int qlzx_go_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_t *dsize, int32_t *status,
                              void *workspace, size_t workspace_bytes, void *stream) {
-    if (int r = check_l1_args(b, status, workspace, workspace_bytes, "qlzx_go_decompress_batch")) return r;
-    if (b->n == 0) return QLZX_R_OK;
-    hipLaunchKernelGGL(qlzx::k_dec_go_l1, dim3((b->n + 63) / 64), dim3(64), 0, (hipStream_t)stream, *b, dst_cap,
-                       dsize, status, (uint8_t *)workspace);
-    HIP_OK(hipGetLastError());
+    if (int r = check_l1_args(b, status, workspace, workspace_bytes, qlzx_go_decompress_workspace_size(b ? b->n : 0),
+                              "qlzx_go_decompress_batch"))
+        return r;
+    for (uint32_t first = 0; first < b->n; first += qlzx::kL1Chunk) {
+        const uint32_t cnt = std::min<uint32_t>(b->n - first, qlzx::kL1Chunk);
+        hipLaunchKernelGGL(qlzx::k_dec_go_l1, dim3((cnt + 63) / 64), dim3(64), 0, (hipStream_t)stream, *b, dst_cap,
+                           dsize, status, (uint8_t *)workspace, first, cnt);
+        HIP_OK(hipGetLastError());
+    }
     return QLZX_R_OK;
 }
 
@@ -341,24 +347,32 @@ struct Ctx {
 };
 thread_local Ctx t_ctx;
 
-}  // namespace
 
-extern "C" {
-
-size_t qlz_compress(const void *source, char *destination, size_t size, char *scratch_compress) {
-    (void)scratch_compress;
-    return qlzx_compress1(source, destination, size, 0);
+// The quicklz.h drop-ins have no error channel: cgo's CCompress ignores a 0 return and keeps an
+// empty Body (quicklz/cquicklz.go:38-40, then store/item.go:145-159 stores it as "compressed"),
+// and crc32_write's result becomes the record CRC (store/crc32.go:81-84).  The reference CPU
+// code cannot fail, so a runtime failure here (no device, a HIP error) stops the process with
+// the reason instead of returning a plausible wrong value.
+[[noreturn]] void die(const char *who) {
+    fprintf(stderr, "libqlzx: %s: %s (GPU runtime failure; the drop-in has no error channel)\n", who,
+            t_last_error.empty() ? "unknown error" : t_last_error.c_str());
+    fflush(stderr);
+    abort();
 }
 
-size_t qlzx_compress1(const void *source, char *destination, size_t size, uint32_t flags) {
-    if (size == 0 || size > 0xffffffffull - 400) return 0;  // quicklz.c:705-706
+thread_local int t_last_status = QLZX_OK;
+
+// One block through the batch encoder.  Returns a qlzx_return code (runtime failure) and sets
+// *csize (0 with t_last_status != OK when the kernel rejects the block).
+int compress1(const void *source, char *destination, size_t size, uint32_t flags, size_t *csize) {
+    *csize = 0;
     Ctx &c = t_ctx;
-    if (c.init()) return 0;
+    if (int r = c.init()) return r;
     const bool l1 = (flags & QLZX_F_LEVEL1) != 0;
     const size_t src_b = align_up(size, 256), dst_b = align_up(size + 400, 256);
     const size_t ws_b = l1 ? qlzx_go_l1_workspace_size(1) : qlzx_compress_workspace_size(1, (uint32_t)size);
     // pinned: [meta | src staging, reused for the result]
-    if (c.reserve(256 + src_b + dst_b + ws_b, 256 + std::max(src_b, dst_b))) return 0;
+    if (int r = c.reserve(256 + src_b + dst_b + ws_b, 256 + std::max(src_b, dst_b))) return r;
     uint8_t *d_meta = c.d_buf, *d_src = d_meta + 256, *d_dst = d_src + src_b, *d_ws = d_dst + dst_b;
     Meta *m = (Meta *)c.h_buf;
     uint8_t *h_data = c.h_buf + 256;
@@ -366,31 +380,39 @@ size_t qlzx_compress1(const void *source, char *destination, size_t size, uint32
     m->src_len = (uint32_t)size;
     memcpy(h_data, source, size);
     // one H2D of descriptor + source (contiguous on both sides)
-    if (hipMemcpyAsync(d_meta, c.h_buf, 256 + size, hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
+    HIP_OK(hipMemcpyAsync(d_meta, c.h_buf, 256 + size, hipMemcpyHostToDevice, c.s));
     Meta *dm = (Meta *)d_meta;
     qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
-    if (l1 ? qlzx_go_l1_compress_batch(&b, &dm->out_size, &dm->status, d_ws, ws_b, c.s)
-           : qlzx_compress_batch(&b, &dm->out_size, &dm->status, nullptr, nullptr, (uint32_t)size, flags, d_ws,
-                                 ws_b, c.s))
-        return 0;
+    if (int r = l1 ? qlzx_go_l1_compress_batch(&b, &dm->out_size, &dm->status, d_ws, ws_b, c.s)
+                   : qlzx_compress_batch(&b, &dm->out_size, &dm->status, nullptr, nullptr, (uint32_t)size, flags,
+                                         d_ws, ws_b, c.s))
+        return r;
     // one D2H of descriptor + the largest possible result, then the only synchronisation
-    if (hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
-    if (hipMemcpyAsync(h_data, d_dst, size + 400, hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
-    if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
-    if (m->status != QLZX_OK || m->out_size == 0 || m->out_size > size + 400) return 0;
+    HIP_OK(hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s));
+    HIP_OK(hipMemcpyAsync(h_data, d_dst, size + 400, hipMemcpyDeviceToHost, c.s));
+    HIP_OK(hipStreamSynchronize(c.s));
+    t_last_status = m->status;
+    if (m->status != QLZX_OK) return QLZX_R_OK;
+    if (m->out_size == 0 || m->out_size > size + 400) return fail(QLZX_R_HIP, "compress1: bad result size");
     memcpy(destination, h_data, m->out_size);
-    return m->out_size;
+    *csize = m->out_size;
+    return QLZX_R_OK;
 }
 
-size_t qlz_decompress(const char *source, void *destination, char *scratch_decompress) {
-    (void)scratch_decompress;
+// One level-3 block through the batch decoder; *dsize = 0 with t_last_status != OK on a
+// corrupt stream.
+int decompress1(const char *source, void *destination, size_t *dsize_out) {
+    *dsize_out = 0;
     const size_t csize = qlz_size_compressed(source), dsize = qlz_size_decompressed(source);
-    if (csize < 3) return 0;
+    if (csize < 3) {
+        t_last_status = QLZX_E_HEADER;
+        return QLZX_R_OK;
+    }
     Ctx &c = t_ctx;
-    if (c.init()) return 0;
+    if (int r = c.init()) return r;
     const size_t src_b = align_up(csize, 256), dst_b = align_up(dsize + 1, 256);
     const size_t ws_b = align_up(qlzx_decompress_workspace_size(1, (uint32_t)dsize), 256);
-    if (c.reserve(256 + src_b + dst_b + ws_b, 256 + std::max(src_b, dst_b))) return 0;
+    if (int r = c.reserve(256 + src_b + dst_b + ws_b, 256 + std::max(src_b, dst_b))) return r;
     uint8_t *d_meta = c.d_buf, *d_src = d_meta + 256, *d_dst = d_src + src_b, *d_ws = d_dst + dst_b;
     Meta *m = (Meta *)c.h_buf;
     uint8_t *h_data = c.h_buf + 256;
@@ -398,33 +420,69 @@ size_t qlz_decompress(const char *source, void *destination, char *scratch_decom
     m->src_len = (uint32_t)csize;
     m->dst_cap = (uint32_t)dsize;
     memcpy(h_data, source, csize);
-    if (hipMemcpyAsync(d_meta, c.h_buf, 256 + csize, hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
+    HIP_OK(hipMemcpyAsync(d_meta, c.h_buf, 256 + csize, hipMemcpyHostToDevice, c.s));
     Meta *dm = (Meta *)d_meta;
     qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
-    if (qlzx_decompress_batch(&b, &dm->dst_cap, &dm->out_size, &dm->status, nullptr, nullptr, nullptr,
-                              (uint32_t)dsize, d_ws, ws_b, c.s))
-        return 0;
-    if (hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
-    if (dsize && hipMemcpyAsync(h_data, d_dst, dsize, hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
-    if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
-    if (m->status != QLZX_OK) return 0;
+    if (int r = qlzx_decompress_batch(&b, &dm->dst_cap, &dm->out_size, &dm->status, nullptr, nullptr, nullptr,
+                                      (uint32_t)dsize, d_ws, ws_b, c.s))
+        return r;
+    HIP_OK(hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s));
+    if (dsize) HIP_OK(hipMemcpyAsync(h_data, d_dst, dsize, hipMemcpyDeviceToHost, c.s));
+    HIP_OK(hipStreamSynchronize(c.s));
+    t_last_status = m->status;
+    if (m->status != QLZX_OK) return QLZX_R_OK;
     memcpy(destination, h_data, dsize);
-    return m->out_size;
+    *dsize_out = m->out_size;
+    return QLZX_R_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qlzx_last_status(void) { return t_last_status; }
+
+size_t qlz_compress(const void *source, char *destination, size_t size, char *scratch_compress) {
+    (void)scratch_compress;
+    if (size == 0 || size > 0xffffffffull - 400) return 0;  // quicklz.c:705-706
+    size_t n = 0;
+    if (compress1(source, destination, size, 0, &n) || n == 0) die("qlz_compress");
+    return n;
+}
+
+size_t qlzx_compress1(const void *source, char *destination, size_t size, uint32_t flags) {
+    if (size == 0 || size > 0xffffffffull - 400) {  // quicklz.c:705-706
+        t_last_status = size ? QLZX_E_TOO_LARGE : QLZX_E_EMPTY;
+        return 0;
+    }
+    size_t n = 0;
+    return compress1(source, destination, size, flags, &n) ? 0 : n;
+}
+
+size_t qlz_decompress(const char *source, void *destination, char *scratch_decompress) {
+    (void)scratch_decompress;
+    size_t n = 0;
+    if (decompress1(source, destination, &n)) die("qlz_decompress");
+    return n;
 }
 
 size_t qlzx_go_decompress1(const char *source, size_t source_len, void *destination, size_t dst_cap) {
-    if (!source || source_len == 0) return 0;
+    if (!source || source_len == 0) {
+        t_last_status = QLZX_E_HEADER;
+        return QLZX_GO_ERROR;
+    }
     const size_t hdr = (source[0] & 2) ? 9 : 3;
     const size_t dsize = source_len >= hdr ? qlz_size_decompressed(source) : 0;  // else the kernel: E_HEADER
     if (dsize > dst_cap) {
+        t_last_status = QLZX_E_DST_CAP;
         fail(QLZX_R_BAD_ARG, "qlzx_go_decompress1: destination too small");
-        return 0;
+        return QLZX_GO_ERROR;
     }
     Ctx &c = t_ctx;
-    if (c.init()) return 0;
+    if (c.init()) return QLZX_GO_ERROR;
     const size_t src_b = align_up(source_len, 256), dst_b = align_up(dsize + 1, 256);
-    const size_t ws_b = qlzx_go_l1_workspace_size(1);
-    if (c.reserve(256 + src_b + dst_b + ws_b, 256 + std::max(src_b, dst_b))) return 0;
+    const size_t ws_b = qlzx_go_decompress_workspace_size(1);
+    if (c.reserve(256 + src_b + dst_b + ws_b, 256 + std::max(src_b, dst_b))) return QLZX_GO_ERROR;
     uint8_t *d_meta = c.d_buf, *d_src = d_meta + 256, *d_dst = d_src + src_b, *d_ws = d_dst + dst_b;
     Meta *m = (Meta *)c.h_buf;
     uint8_t *h_data = c.h_buf + 256;
@@ -432,40 +490,49 @@ size_t qlzx_go_decompress1(const char *source, size_t source_len, void *destinat
     m->src_len = (uint32_t)source_len;
     m->dst_cap = (uint32_t)dsize;
     memcpy(h_data, source, source_len);
-    if (hipMemcpyAsync(d_meta, c.h_buf, 256 + source_len, hipMemcpyHostToDevice, c.s) != hipSuccess) return 0;
+    if (hipMemcpyAsync(d_meta, c.h_buf, 256 + source_len, hipMemcpyHostToDevice, c.s) != hipSuccess)
+        return fail(QLZX_R_HIP, "qlzx_go_decompress1: H2D"), QLZX_GO_ERROR;
     Meta *dm = (Meta *)d_meta;
     qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
-    if (qlzx_go_decompress_batch(&b, &dm->dst_cap, &dm->out_size, &dm->status, d_ws, ws_b, c.s)) return 0;
-    if (hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
-    if (dsize && hipMemcpyAsync(h_data, d_dst, dsize, hipMemcpyDeviceToHost, c.s) != hipSuccess) return 0;
-    if (hipStreamSynchronize(c.s) != hipSuccess) return 0;
+    if (qlzx_go_decompress_batch(&b, &dm->dst_cap, &dm->out_size, &dm->status, d_ws, ws_b, c.s)) return QLZX_GO_ERROR;
+    if (hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess ||
+        (dsize && hipMemcpyAsync(h_data, d_dst, dsize, hipMemcpyDeviceToHost, c.s) != hipSuccess) ||
+        hipStreamSynchronize(c.s) != hipSuccess)
+        return fail(QLZX_R_HIP, "qlzx_go_decompress1: D2H"), QLZX_GO_ERROR;
+    t_last_status = m->status;
     if (m->status != QLZX_OK) {
         char msg[64];
         snprintf(msg, sizeof msg, "qlzx_go_decompress1: status %d", (int)m->status);
-        fail(QLZX_R_BAD_ARG, msg);
-        return 0;
+        fail(QLZX_R_OK, msg);
+        return QLZX_GO_ERROR;
     }
     memcpy(destination, h_data, dsize);
-    return dsize ? dsize : 0;
+    return dsize;
 }
 
 uint32_t crc32_write(uint32_t crc, unsigned char *buf, int len) {
     if (len <= 0) return crc;  // store/crc32.go:65 loops zero times
     Ctx &c = t_ctx;
-    if (c.init()) return crc;
+    if (c.init()) die("crc32_write");
     const size_t src_b = align_up((size_t)len, 256);
-    if (c.reserve(256 + src_b, 256 + src_b)) return crc;
+    if (c.reserve(256 + src_b, 256 + src_b)) die("crc32_write");
     uint8_t *d_meta = c.d_buf, *d_src = d_meta + 256;
     Meta *m = (Meta *)c.h_buf;
     memset(m, 0, sizeof(Meta));
     m->src_len = (uint32_t)len;
     m->crc_in = crc;
     memcpy(c.h_buf + 256, buf, (size_t)len);
-    if (hipMemcpyAsync(d_meta, c.h_buf, 256 + (size_t)len, hipMemcpyHostToDevice, c.s) != hipSuccess) return crc;
     Meta *dm = (Meta *)d_meta;
-    if (qlzx_crc32_batch(d_src, &dm->src_off, &dm->src_len, 1, &dm->crc_in, 0, &dm->crc_out, c.s)) return crc;
-    if (hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s) != hipSuccess) return crc;
-    if (hipStreamSynchronize(c.s) != hipSuccess) return crc;
+    hipError_t e = hipMemcpyAsync(d_meta, c.h_buf, 256 + (size_t)len, hipMemcpyHostToDevice, c.s);
+    if (e == hipSuccess &&
+        qlzx_crc32_batch(d_src, &dm->src_off, &dm->src_len, 1, &dm->crc_in, 0, &dm->crc_out, c.s) != QLZX_R_OK)
+        die("crc32_write");
+    if (e == hipSuccess) e = hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s);
+    if (e == hipSuccess) e = hipStreamSynchronize(c.s);
+    if (e != hipSuccess) {
+        fail(QLZX_R_HIP, "crc32_write", e);
+        die("crc32_write");
+    }
     return m->crc_out;
 }
 

@@ -21,7 +21,7 @@
 //
 // As the batch path for 16 KiB blocks it is 3.4x slower than K1/K2 (every
 // lane's recent output competes for L2), so it serves the large
-// values only; QLZX_DECODE=lane8 routes whole batches here for experiments.
+// values only, and every block of a batch given no workspace.
 #include "qlzx_device.h"
 
 namespace qlzx {
@@ -30,7 +30,8 @@ __device__ __forceinline__ uint64_t ldu64(const uint8_t *p) { return *(const uin
 __device__ __forceinline__ void stu64(uint8_t *p, uint64_t v) { *(uint64_t *)p = v; }
 __device__ __forceinline__ uint32_t ldu32(const uint8_t *p) { return *(const uint32_t *)p; }
 
-__device__ int decode_lane8(const uint8_t *src, uint32_t len, uint8_t *dst, uint64_t cap, uint32_t &dsize_out) {
+__device__ int decode_lane8(const uint8_t *src, uint32_t len, uint8_t *dst, uint64_t cap, uint32_t max_dsize,
+                            uint32_t &dsize_out) {
     dsize_out = 0;
     if (len < 3) return QLZX_E_HEADER;
     const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
@@ -39,6 +40,7 @@ __device__ int decode_lane8(const uint8_t *src, uint32_t len, uint8_t *dst, uint
     if (h.csize != len) return QLZX_E_SIZE_COMPRESSED;
     if (h.level != 3) return QLZX_E_LEVEL;
     if ((uint64_t)h.dsize > cap) return QLZX_E_DST_CAP;
+    if (h.dsize > max_dsize) return QLZX_E_MAX_DSIZE;  // K1's order of checks
     const uint32_t csize = h.csize, dsize = h.dsize;
     if (!h.compressed) {  // stored block (quicklz.c:808-811)
         if ((uint64_t)csize < (uint64_t)hdr + dsize) return QLZX_E_CORRUPT;
@@ -108,14 +110,14 @@ __device__ int decode_lane8(const uint8_t *src, uint32_t len, uint8_t *dst, uint
     return QLZX_OK;
 }
 
-// Handles blocks with dsize >= min_dsize (smaller ones belong to the fast path
-// when it runs; min_dsize = 0 -> all).  min_dsize = kLane8Pending: only the fast-path-sized
-// blocks K1 left to this kernel (status kPending: a literal run too long for k_dec_seq).
-constexpr uint32_t kLane8Pending = 0xFFFFFFFFu;
+// Handles blocks with min_dsize <= dsize (smaller ones belong to the fast path when it
+// runs; min_dsize = 0 -> all).  A block whose header dsize exceeds the caller's max_dsize is
+// not decoded: QLZX_E_MAX_DSIZE (include/qlzx.h, the batch contract), so a caller that sizes
+// its destinations by max_dsize is never written past them.
 __global__ void __launch_bounds__(256) k_dec_lane8(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize,
                                                    int32_t *status, const uint32_t *crc_state,
                                                    const uint32_t *crc_expect, uint32_t *crc_out,
-                                                   uint32_t min_dsize) {
+                                                   uint32_t min_dsize, uint32_t max_dsize) {
     __shared__ uint32_t tab[256];
     load_crc_table(tab);
     __syncthreads();
@@ -123,13 +125,10 @@ __global__ void __launch_bounds__(256) k_dec_lane8(qlzx_blocks b, const uint32_t
     if (i >= b.n) return;
     const uint8_t *src = b.src + b.src_off[i];
     const uint32_t len = b.src_len[i];
-    if (min_dsize == kLane8Pending) {
-        if (status[i] != kPending || len < 3) return;
+    if (min_dsize) {  // header errors of fast-path batches are reported by K1
+        if (len < 3) return;
         const uint32_t hb = (src[0] & 2u) ? 9u : 3u;
-        if (len < hb || parse_header(src).dsize > QLZX_FAST_MAX_DSIZE) return;
-    } else if (min_dsize && len >= 3) {
-        const uint32_t hb = (src[0] & 2u) ? 9u : 3u;
-        if (len >= hb && parse_header(src).dsize < min_dsize) return;  // owned by the fast path
+        if (len < hb || parse_header(src).dsize < min_dsize) return;  // owned by the fast path
     }
     int st = QLZX_OK;
     if (crc_state || crc_expect || crc_out) {  // record CRC over the stored (compressed) value bytes
@@ -142,7 +141,7 @@ __global__ void __launch_bounds__(256) k_dec_lane8(qlzx_blocks b, const uint32_t
         if (crc_expect && c != crc_expect[i]) st = QLZX_E_CRC;  // store/datafile.go:161-168: before decode
     }
     uint32_t ds = 0;
-    if (st == QLZX_OK) st = decode_lane8(src, len, b.dst + b.dst_off[i], dst_cap ? dst_cap[i] : ~0ull, ds);
+    if (st == QLZX_OK) st = decode_lane8(src, len, b.dst + b.dst_off[i], dst_cap ? dst_cap[i] : ~0ull, max_dsize, ds);
     if (dsize) dsize[i] = ds;
     status[i] = st;
 }

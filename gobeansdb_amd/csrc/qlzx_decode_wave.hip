@@ -48,6 +48,7 @@ struct GroupRec {
 };
 
 constexpr int32_t kPending = -1;  // status of blocks left to the general path
+constexpr uint32_t kMaxDevices = 64;  // per-device side streams of the launcher
 constexpr uint32_t kBlkSkip = 0, kBlkStored = 1, kBlkCompressed = 2;
 // K1 workgroup: one wave (the 16 KiB LDS ring per wave bounds occupancy); with the CRC,
 // four waves share one 8 KiB slicing-by-8 table (8 waves/CU instead of 6)
@@ -85,23 +86,7 @@ static_assert(QLZX_K2_VMWAIT == 2 * QLZX_K2_SLACK,
 
 __host__ __device__ inline uint32_t groups_max(uint32_t max_dsize) { return max_dsize / 31u + 2u; }
 
-inline bool decode_wave_enabled() { return true; }
-
-// K2 kernel of this process: QLZX_K2 = (unset) | split | seq; read per call, so tests can
-// run every kernel in one process.  Only seq changes the workspace (match records).
-enum K2Mode { kK2Items = 0, kK2Split = 1, kK2Seq = 2 };
-inline K2Mode k2_mode() {
-    const char *e = getenv("QLZX_K2");
-    return !e ? kK2Items : !strcmp(e, "split") ? kK2Split : !strcmp(e, "seq") ? kK2Seq : kK2Items;
-}
-
-// per-block record area in whole GroupRecs: group records (K2, split K2), or with
-// QLZX_K2=seq the match records of k_dec_seq (u32 per match, up to dsize/3 + 2: 2.6x more)
-inline size_t rec_bytes_max(uint32_t md) {
-    const uint32_t seq_units = (4u * (md / 3u + 2u) + sizeof(GroupRec) - 1) / sizeof(GroupRec);
-    const uint32_t units = k2_mode() == kK2Seq && seq_units > groups_max(md) ? seq_units : groups_max(md);
-    return (size_t)units * sizeof(GroupRec);
-}
+inline size_t rec_bytes_max(uint32_t md) { return (size_t)groups_max(md) * sizeof(GroupRec); }
 
 inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
     const uint32_t md = max_dsize > QLZX_FAST_MAX_DSIZE ? QLZX_FAST_MAX_DSIZE : max_dsize;
@@ -209,33 +194,19 @@ __device__ __forceinline__ void ring_issue(uint8_t *ring_wave, const uint8_t *gb
     }
 }
 
-// SEQ (K2 = k_dec_seq, qlzx_decode_seq.hip): instead of group records, one u32 per match,
-// I | X << 16 (I = item index, X = token bytes beyond the first of the matches before it, so
-// the token sits at hdr + 4 (I / 31 + 1) + I + X), `recs` read as u32[mcap] per block.  Such a
-// record needs I < 65536 and X < 65536, true of every valid stream of dsize <= 64 KiB (a match
-// emits >= 3 bytes, so #matches <= dsize / 3); the block is E_CORRUPT otherwise.  A literal run
-// of more than kSeqRunMax items leaves the block to the general path (kPending), so one K2
-// sequence (run + match) always fits half the output window.
-constexpr uint32_t kSeqRunMax = 1024;
-__host__ __device__ inline uint32_t seq_mcap(uint32_t max_dsize) { return max_dsize / 3u + 2u; }
-
-template <bool CRC, bool SEQ = false>
+template <bool CRC>
 __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, const uint32_t *dst_cap,
                                                          uint32_t *dsize_out, int32_t *status,
                                                          const uint32_t *crc_state, const uint32_t *crc_expect,
                                                          uint32_t *crc_out, uint32_t first, uint32_t count,
                                                          BlkInfo *info, GroupRec *recs, uint32_t gmax,
-                                                         const uint32_t *order, uint32_t max_dsize,
-                                                         uint32_t mcap = 0) {
+                                                         const uint32_t *order, uint32_t max_dsize) {
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG<CRC> / 64) * kRingWave];
     __shared__ uint32_t tab[CRC ? 8 * 256 : 1];
     if (CRC) {
         for (uint32_t t = threadIdx.x; t < 8 * 256; t += kParseWG<CRC>) tab[t] = g_crc_slice8[t];
         __syncthreads();
     }
-#if QLZX_K1_PRIO > 0
-    __builtin_amdgcn_s_setprio(QLZX_K1_PRIO);  // experiments: K1 waves above K2's in issue arbitration
-#endif
     const uint32_t lane = threadIdx.x & 63;
     uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWave;
     const uint32_t lin = blockIdx.x * kParseWG<CRC> + threadIdx.x;
@@ -281,8 +252,6 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
     // parse state
     uint32_t ip = hdr, g = 0, k = 31, cw = 0, m = 0, ra = 0, rb = 0, rec_ip = 0;
     GroupRec *myrec = recs + (size_t)(inrange ? lin : 0) * gmax;
-    uint32_t *mrec = (uint32_t *)recs + (size_t)(inrange ? lin : 0) * mcap;
-    uint32_t jm = 0, lit = 0;  // SEQ: match records written; literal items since the last match
     uint32_t crc = (CRC && inrange && crc_state) ? crc_state[i] : 0xffffffffu;
     bool done_parse = !parsing;
 
@@ -353,24 +322,8 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
             bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) |  // C1, group bound
                                    (mat & (ipm + code + 1 > csize)) |        // C2
                                    (mat2 & (ip2 + code2 + 1 > csize)));
-            bool pend = false;
-            if (SEQ) {
-                const uint32_t I1 = 31u * (g - 1u) + km, X1 = ipm - hdr - 4u * g - I1;
-                bad = bad | (stepping & mat & ((I1 >= dsize) | (X1 + (mat2 ? code : 0u) > 0xFFFFu) |
-                                               (jm + (mat2 ? 2u : 1u) > mcap)));
-                pend = stepping & !bad & mat & (lit + run > kSeqRunMax);
-                if (stepping & !bad & !pend & mat) {
-                    mrec[jm] = I1 | (X1 << 16);
-                    if (mat2) mrec[jm + 1] = (I1 + 1u) | ((X1 + code) << 16);
-                }
-            } else if (stepping & gb & (g > 0)) {
-                myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
-            }
-            if (SEQ) {
-                st = pend ? kPending : st;
-                bad = bad | pend;  // stops the parse like an error (the status stays kPending)
-            }
-            st = (bad & !pend) ? QLZX_E_CORRUPT : st;
+            if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
+            st = bad ? QLZX_E_CORRUPT : st;
             const bool adv = stepping & !bad;
             const bool ag = adv & gb;
             const uint32_t bm = mat ? (1u << (km & 31)) : 0u;
@@ -383,10 +336,6 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
             m = adv ? (gb ? 0u : m | bm | bm2) : m;
             ra = adv ? (gb ? 0u : ra | ((code & 1u) ? bm : 0u) | ((code2 & 1u) ? bm2 : 0u)) : ra;
             rb = adv ? (gb ? 0u : rb | ((code & 2u) ? bm : 0u) | ((code2 & 2u) ? bm2 : 0u)) : rb;
-            if (SEQ) {
-                jm += (adv & mat) ? (mat2 ? 2u : 1u) : 0u;
-                lit = (adv & !gb) ? (mat ? 0u : lit + run) : lit;
-            }
             done_parse = done_parse | (go & (end | bad));
             go = adv;
         }
@@ -396,12 +345,11 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
         ring_issue(ring, gbase, dummy, r + 3, last16, stream && r + 3 <= last_round);
     }
     PROF_MARK(4);  // 4: DMA issue + loop overhead
-    if (!SEQ && parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
+    if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
     PROF_FLUSH(0);
     vm_sync();
     if (!inrange) return;
     if (st == QLZX_OK && kind == kBlkCompressed && (!done_parse || g == 0)) st = QLZX_E_CORRUPT;
-    if (SEQ && st == QLZX_OK && kind == kBlkCompressed && lit > kSeqRunMax) st = kPending;  // trailing run
     if (CRC) {
         const uint32_t c = ~crc;
         if (crc_out) crc_out[i] = c;
@@ -415,10 +363,6 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
     } else if (kind == kBlkCompressed) {
         bi.ngroups = g;
         bi.nitems = (g - 1) * 31 + (k > 31 ? 31 : k);
-        if (SEQ) {  // ngroups -> match count; kind | (X after the last match) << 8 (<= 65535 + 3)
-            bi.ngroups = jm;
-            bi.kind = kind | ((ip - hdr - 4u * g - bi.nitems) << 8);
-        }
     }
     info[lin] = bi;
 }
@@ -429,11 +373,7 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
 template <uint32_t OFF = 0>
 __device__ __forceinline__ void lds_mskor(uint32_t *addr, uint32_t mask, uint32_t val) {
     const uint32_t a = (uint32_t)(uintptr_t)addr;
-#ifdef QLZX_EXP_PLAINWRITE  // experiment: plain dword stores (wrong bytes; timing only)
-    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(a), "v"(val | mask), "i"(OFF) : "memory");
-#else
     asm volatile("ds_mskor_b32 %0, %1, %2 offset:%3" ::"v"(a), "v"(mask), "v"(val), "i"(OFF) : "memory");
-#endif
 }
 
 // K2 shared memory: prefetch slots, then the output window.  Output position
@@ -638,68 +578,24 @@ __device__ __forceinline__ uint32_t ff1_or(uint64_t m, uint32_t dflt) {
 // Far source (below the window): the five destination-aligned dwords
 // y[j] = bytes [a0 + 4j, a0 + 4j + 4) of the block's output in HBM, a0 = s - lo
 // (lo = the destination's byte offset in its dword, whose lo leading bytes the
-// caller masks off; callers guarantee s >= lo).  Unaligned dword loads straight
-// into y (no shuffle), so nothing waits on them until the first sub-round.
-// Dwords that hold needed bytes end <= d + 3 < dsize (check C3); later ones are
-// clamped inside [0, lim) and masked off.
-__device__ __forceinline__ void far_load20(const uint8_t *dst, uint32_t a0, uint32_t lim, uint32_t y[5]) {
-#pragma unroll
-    for (int j = 0; j < 5; j++) {
-        uint32_t a = a0 + 4 * j;
-        a = a + 4 <= lim ? a : lim - 4;
-        y[j] = *(const uint32_t *)(dst + a);  // unaligned dword load (unaligned access mode)
-    }
-}
-
-// K2's far loads when a0 + 20 <= the block's dsize (the caller checks base + 20 <= dsize: a far
-// source lies below base), so no per-dword clamp: five unaligned dword loads (unaligned access
-// mode).
-// QLZX_K2_FARFAST=1 (default): far loads without the per-dword clamp; while the window base is
-// within 20 B of the block's end, far lanes take the byte path instead (c2 38.09 -> 37.79 ms).
-// Merged 16-B far loads (FAR_W=16) measured the same; a per-lane clamp/fast branch needed 66
-// VGPRs (7 waves/SIMD) and lost.
-#ifndef QLZX_K1_PRIO
-#define QLZX_K1_PRIO 0
-#endif
-#ifndef QLZX_K2_PRIO
-#define QLZX_K2_PRIO 0
-#endif
-#ifndef QLZX_K2_FARFAST
-#define QLZX_K2_FARFAST 1
-#endif
-#ifndef QLZX_K2_FAR_W
-#define QLZX_K2_FAR_W 1
-#endif
+// caller masks off; callers guarantee s >= lo), as unaligned dword loads straight into y
+// (no shuffle), so nothing waits on them until the first sub-round.  A far source ends
+// below base, so the 20-B read stays inside the block while base + 20 <= dsize (no
+// per-dword clamp); otherwise far lanes take the byte path.
+// Five dword loads from opaque offsets: merged loads need aligned register tuples (66 VGPRs).
+// While the window base is within 20 B of the block's end, far lanes take the byte path instead
+// (c2 38.09 -> 37.79 ms against a per-dword clamp).
 __device__ __forceinline__ void far_load20_fast(const uint8_t *dst, uint32_t a0, uint32_t y[5]) {
-#if QLZX_K2_FAR_W == 8
-    const uint8_t *p = dst + a0;
-    const uint2 u = *(const uint2 *)p, v = *(const uint2 *)(p + 8);
-    y[0] = u.x, y[1] = u.y, y[2] = v.x, y[3] = v.y;
-    y[4] = *(const uint32_t *)(p + 16);
-#elif QLZX_K2_FAR_W == 16
-    const uint8_t *p = dst + a0;
-    const uint4 u = *(const uint4 *)p;
-    y[0] = u.x, y[1] = u.y, y[2] = u.z, y[3] = u.w;
-    y[4] = *(const uint32_t *)(p + 16);
-#elif QLZX_K2_FAR_W == 4
-    const uint32_t *q = (const uint32_t *)(dst + a0);
-    y[0] = q[0], y[1] = q[1], y[2] = q[2], y[3] = q[3], y[4] = q[4];
-#else  // five dword loads from opaque offsets: merged loads need aligned register tuples (66 VGPRs)
 #pragma unroll
     for (int j = 0; j < 5; j++) {
         uint32_t a = a0 + 4 * j;
         asm volatile("" : "+v"(a));
         y[j] = *(const uint32_t *)(dst + a);
     }
-#endif
 }
 
-#ifndef QLZX_K2_WAVES_PER_EU
-#define QLZX_K2_WAVES_PER_EU 1
-#endif
 template <uint32_t W>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLZX_K2_WAVES_PER_EU)))
-k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
+__global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                                                    uint32_t first, uint32_t count, const BlkInfo *info,
                                                    const GroupRec *recs, uint32_t gmax, const uint32_t *list) {
     static_assert(W % 2048 == 0 && W >= 2048, "window: a multiple of 2 KiB (slides by W/2)");
@@ -707,11 +603,6 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
     const uint32_t lane = threadIdx.x;
     const uint32_t bx = blockIdx.x;  // workspace slot
     if (bx >= count) return;
-#if QLZX_K2_PRIO > 0
-    // K2 waves above K1's (priority 0) in the SIMD's issue arbitration: K1 of the next chunk,
-    // which has the whole K2 to hide under, takes the slots K2 leaves idle
-    __builtin_amdgcn_s_setprio(QLZX_K2_PRIO);
-#endif
     const uint32_t i = list ? list[bx] : first + bx;  // block
     const BlkInfo bi = info[bx];
     if (bi.kind == kBlkSkip) return;
@@ -827,26 +718,18 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             // far sources (below the window, already in HBM): load them first, use them in the first sub-round
             const uint32_t s = d - off;
             const bool far = s < base;
-            // byte / chunked path; with FARFAST also every far source while the window base is within 20 B
+            // byte / chunked path; also every far source while the window base is within 20 B
             // of the block's end (wave-uniform, rare), so far_load20_fast never reads past dsize
-            const bool nearend = QLZX_K2_FARFAST && base + 20 > dsize;
+            const bool nearend = base + 20 > dsize;
             const bool spec = off < len || len > 16 || (far && (s + len > base || s < 3 || nearend));
             // only read under fc, which implies fload: no zero fill, whose register writes made
             // the compiler wait (vmcnt) for every load still in flight, prefetch DMAs included
             uint32_t fy[5];
-#ifdef QLZX_EXP_NOFAR  // experiment: far sources read garbage from LDS (timing only)
-            const bool fload = false;
-#else
             const bool fload = in && valid && ism && far && !spec;
-#endif
             if (__ballot(fload)) {
                 // a far source ends below base: its 20-B read stays inside the block unless the
-                // window base is within 20 B of the end (FARFAST: then those lanes are spec)
-#if QLZX_K2_FARFAST
+                // window base is within 20 B of the end (then those lanes are spec)
                 if (fload) far_load20_fast(dst, s - (d & 3u), fy);
-#else
-                if (fload) far_load20(dst, s - (d & 3u), dsize, fy);
-#endif
             }
             // ---- checks C2-C5 on the live items (those that start before dsize) ----
             const bool live = in && valid && d < dsize;
@@ -904,12 +787,10 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             PROF_MARK(7);  // 7: far copies (waits for the far loads)
             uint64_t pend = __ballot(!done);
             const bool spec_any = __ballot(!done && spec) != 0;  // rare: skip its test per sub-round
-#ifndef QLZX_K2_CLOOP
             if (!spec_any) {  // every pending match takes the 16-B copy: the hand-scheduled loop
                 if (pend) subrounds_plain(pend, need, cp, win);
                 pend = 0;
             }
-#endif
             while (pend) {
                 // exact: every byte of the source is final once none of the lanes owning it is pending
                 const bool ready = !done & ((need & pend) == 0);
@@ -932,10 +813,6 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                         }
                     }
                 }
-#ifdef QLZX_EXP_ONESUB  // experiment: every pending match copies in the first sub-round (timing only)
-                if (!ready && !done && !spec) cp.run(win);
-                done = true;
-#endif
                 done = done || ready;
                 // no lgkmcnt wait: a wave's LDS operations execute in issue order, so the
                 // next sub-round's reads observe these writes
@@ -946,20 +823,6 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
             if (__ballot(err)) { more = false; complete = false; }
         }
         if (__ballot(err)) break;
-#ifdef QLZX_EXP_PADV  // experiment: extra dependent VALU per batch (issue-bound test; timing only)
-        {
-            uint32_t x = lane;
-            for (int j = 0; j < QLZX_EXP_PADV; j++) asm volatile("v_add_u32 %0, %0, 1" : "+v"(x));
-            asm volatile("" ::"v"(x));
-        }
-#endif
-#ifdef QLZX_EXP_PADS  // experiment: extra dependent SALU per batch
-        {
-            uint32_t x = bt;
-            for (int j = 0; j < QLZX_EXP_PADS; j++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(x)::"scc");
-            asm volatile("" ::"s"(x));
-        }
-#endif
         // the records of batch bt+kRecAhead, issued after this iteration's far loads were consumed:
         // a DMA issued before them is in the in-order vmcnt queue ahead of them, so the far-load
         // wait would also wait for it (c2: 41.0-41.4 -> 39.7-40.2 ms with the fy change above)
@@ -990,6 +853,94 @@ k_dec_blocks(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
         status[i] = QLZX_OK;
         if (dsize_out) dsize_out[i] = dsize;
     }
+}
+
+inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uint32_t *dsize,
+                              int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
+                              uint32_t *crc_out, uint32_t max_dsize, void *ws, size_t ws_bytes,
+                              hipStream_t s) {
+    const uint32_t md = max_dsize > QLZX_FAST_MAX_DSIZE ? QLZX_FAST_MAX_DSIZE : max_dsize;
+    const uint32_t gmax = groups_max(md);
+    const uint32_t chunk = b.n < kChunkBlocks ? b.n : kChunkBlocks;
+    const size_t o_rec = ((size_t)chunk * sizeof(BlkInfo) + 255) & ~(size_t)255;
+    const size_t one = decode_wave_ws_bytes(b.n, max_dsize);
+    const size_t o_list = o_rec + ((((size_t)chunk * rec_bytes_max(md)) + 255) & ~(size_t)255);
+    const size_t o_aux = o_list + ((((size_t)b.n * sizeof(uint32_t)) + 255) & ~(size_t)255);
+    const bool sort = chunk > 64;
+    // two workspace halves when the caller gave room for them: K1 of chunk c+1 runs on a
+    // side stream while K2 of chunk c runs on `s` (K1 is latency-bound at low occupancy)
+    const bool overlap = ws_bytes >= 2 * one && b.n > chunk;
+    // per host thread (the batch API is re-entrant like the reference) and per device: the
+    // side stream and events are created on the device that owns `s`
+    struct Side {
+        hipStream_t st = nullptr;
+        hipEvent_t k1[2], k2[2];
+    };
+    thread_local Side sides[kMaxDevices];
+    hipStream_t side = nullptr;
+    hipEvent_t *ev_k1 = nullptr, *ev_k2 = nullptr;
+    if (overlap) {
+        int dev = 0, cur = 0;
+        if (s) {
+            hipDevice_t hd;
+            if (hipStreamGetDevice(s, &hd) != hipSuccess) return (int)hipErrorInvalidResourceHandle;
+            dev = (int)hd;
+        } else if (hipGetDevice(&dev) != hipSuccess) {
+            return (int)hipErrorNoDevice;
+        }
+        if (dev < 0 || dev >= (int)kMaxDevices) return (int)hipErrorInvalidDevice;
+        Side &sd = sides[dev];
+        if (!sd.st) {
+            (void)hipGetDevice(&cur);
+            if (cur != dev) (void)hipSetDevice(dev);
+            hipError_t e = hipStreamCreateWithFlags(&sd.st, hipStreamNonBlocking);
+            for (int j = 0; j < 2 && e == hipSuccess; j++) {
+                e = hipEventCreateWithFlags(&sd.k1[j], hipEventDisableTiming);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&sd.k2[j], hipEventDisableTiming);
+            }
+            if (cur != dev) (void)hipSetDevice(cur);
+            if (e != hipSuccess) return (int)e;
+        }
+        side = sd.st;
+        ev_k1 = sd.k1;
+        ev_k2 = sd.k2;
+    }
+    const bool crc = crc_state || crc_expect || crc_out;
+    if (overlap) (void)hipEventRecord(ev_k2[1], s), (void)hipStreamWaitEvent(side, ev_k2[1], 0);
+    if (sort) {  // block order of the whole call, ahead of the first K1 (workspace half 0)
+        hipStream_t s1 = overlap ? side : s;
+        uint32_t *aux = (uint32_t *)((uint8_t *)ws + o_aux);
+        (void)hipMemsetAsync(aux, 0, kOrderAux * sizeof(uint32_t), s1);
+        const dim3 g((b.n + kOrderPerWG - 1) / kOrderPerWG);
+        hipLaunchKernelGGL(k_order_count, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, aux);
+        hipLaunchKernelGGL(k_order_scatter, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, aux,
+                           (uint32_t *)((uint8_t *)ws + o_list));
+    }
+    uint32_t c = 0;
+    for (uint32_t first = 0; first < b.n; first += chunk, c++) {
+        const uint32_t cnt = b.n - first < chunk ? b.n - first : chunk;
+        uint8_t *w = (uint8_t *)ws + (overlap ? (c & 1) * one : 0);
+        BlkInfo *info = (BlkInfo *)w;
+        GroupRec *recs = (GroupRec *)(w + o_rec);
+        uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
+        hipStream_t s1 = overlap ? side : s;
+        if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
+        const dim3 g1c((cnt + kParseWG<true> - 1) / kParseWG<true>), g1((cnt + kParseWG<false> - 1) / kParseWG<false>);
+        if (crc)
+            hipLaunchKernelGGL((k_dec_parse<true>), g1c, dim3(kParseWG<true>), 0, s1, b, dst_cap, dsize, status,
+                               crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order, max_dsize);
+        else
+            hipLaunchKernelGGL((k_dec_parse<false>), g1, dim3(kParseWG<false>), 0, s1, b, dst_cap, dsize, status,
+                               crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order, max_dsize);
+        if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
+        // one kernel for every block size: the LDS window slides over longer blocks
+        hipLaunchKernelGGL(k_dec_blocks<kWin>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info, recs,
+                           gmax, (const uint32_t *)order);
+        if (overlap) (void)hipEventRecord(ev_k2[c & 1], s);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+    }
+    return 0;
 }
 
 }  // namespace qlzx

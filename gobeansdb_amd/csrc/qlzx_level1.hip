@@ -22,6 +22,10 @@ namespace qlzx {
 constexpr uint32_t kL1Hash = 4096;
 // per-block workspace: u32 hashtable[4096] | u32 cachetable[4096] | u8 counter[4096]
 constexpr size_t kL1WsBlock = 2 * 4 * kL1Hash + kL1Hash;
+// the decoder uses only the hashtable
+constexpr size_t kL1DecWsBlock = 4 * kL1Hash;
+// launches cover at most this many blocks, reusing one bounded workspace chunk after chunk
+constexpr uint32_t kL1Chunk = 65536;
 
 __device__ __forceinline__ uint32_t l1_bucket(uint32_t f) { return ((f >> 12) ^ f) & (kL1Hash - 1); }
 __device__ __forceinline__ uint32_t l1_rd3(const uint8_t *s, int64_t i) {
@@ -45,9 +49,10 @@ __device__ void l1_zero(uint8_t *p, uint64_t n) {
 }
 
 __global__ void __launch_bounds__(64) k_dec_go_l1(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
-                                                  int32_t *status, uint8_t *ws) {
-    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= b.n) return;
+                                                  int32_t *status, uint8_t *ws, uint32_t first, uint32_t count) {
+    const uint32_t li = blockIdx.x * 64 + threadIdx.x;
+    if (li >= count) return;
+    const uint32_t i = first + li;
     const uint8_t *s = b.src + b.src_off[i];
     uint8_t *dst = b.dst + b.dst_off[i];
     const int64_t n = b.src_len[i];
@@ -72,7 +77,7 @@ __global__ void __launch_bounds__(64) k_dec_go_l1(qlzx_blocks b, const uint32_t 
             st = QLZX_E_LEVEL;  // compressed level 3: qlzx_decompress_batch's
         } else {
             l1_zero(dst, (uint64_t)size);
-            uint32_t *ht = (uint32_t *)(ws + (size_t)i * kL1WsBlock);
+            uint32_t *ht = (uint32_t *)(ws + (size_t)li * kL1DecWsBlock);
             for (uint32_t q = 0; q < kL1Hash; q += 4) *(uint4 *)(ht + q) = make_uint4(0, 0, 0, 0);
             int64_t src = hdr, d = 0, last_hashed = -1;
             const int64_t last_match_start = size - 11;
@@ -158,9 +163,11 @@ __global__ void __launch_bounds__(64) k_dec_go_l1(qlzx_blocks b, const uint32_t 
 
 // Go Compress(src, 1).  dst capacity >= len + 400 (quicklz.go:84); empty input: QLZX_E_EMPTY
 // (Go returns nil).
-__global__ void __launch_bounds__(64) k_enc_go_l1(qlzx_blocks b, uint32_t *csize, int32_t *status, uint8_t *ws) {
-    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= b.n) return;
+__global__ void __launch_bounds__(64) k_enc_go_l1(qlzx_blocks b, uint32_t *csize, int32_t *status, uint8_t *ws,
+                                                  uint32_t first, uint32_t count) {
+    const uint32_t li = blockIdx.x * 64 + threadIdx.x;
+    if (li >= count) return;
+    const uint32_t i = first + li;
     const uint8_t *s = b.src + b.src_off[i];
     uint8_t *d = b.dst + b.dst_off[i];
     const int64_t len = b.src_len[i];
@@ -169,7 +176,7 @@ __global__ void __launch_bounds__(64) k_enc_go_l1(qlzx_blocks b, uint32_t *csize
         if (status) status[i] = QLZX_E_EMPTY;
         return;
     }
-    uint32_t *ht = (uint32_t *)(ws + (size_t)i * kL1WsBlock);
+    uint32_t *ht = (uint32_t *)(ws + (size_t)li * kL1WsBlock);
     uint32_t *cache_t = ht + kL1Hash;
     uint8_t *counter = (uint8_t *)(cache_t + kL1Hash);
     for (uint32_t q = 0; q < 2 * kL1Hash + kL1Hash / 4; q += 4) *(uint4 *)(ht + q) = make_uint4(0, 0, 0, 0);

@@ -130,12 +130,18 @@ def Decompress(source) -> bytes:
         raise QuicklzError("Go version only supports level 1 and 3")
     n = SizeDecompressed(s)
     dst = ctypes.create_string_buffer(max(n, 1))
+    L = _lib.lib()
     if level == 3 and (s[0] & 1):
-        size = _lib.lib().qlz_decompress(s, dst, None)
+        size = L.qlz_decompress(s, dst, None)
+        bad = size != n or L.qlzx_last_status() != _lib.OK
     else:
-        size = _lib.lib().qlzx_go_decompress1(s, len(s), dst, n)
-    if size != n:
-        raise QuicklzError(f"corrupt quicklz stream (status {_lib.lib().qlzx_last_error().decode()})")
+        # QLZX_GO_ERROR is the error channel: a dsize-0 stream the kernel rejects must raise too
+        size = L.qlzx_go_decompress1(s, len(s), dst, n)
+        bad = size == _lib.GO_ERROR or size != n
+    if bad:
+        st = L.qlzx_last_status()
+        name = _lib.STATUS_NAMES[st] if 0 <= st < len(_lib.STATUS_NAMES) else str(st)
+        raise QuicklzError(f"corrupt quicklz stream (status {name}: {L.qlzx_last_error().decode()})")
     return dst.raw[:n]
 
 

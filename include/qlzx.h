@@ -38,7 +38,12 @@ size_t qlz_size_decompressed(const char *source);
 size_t qlz_size_compressed(const char *source);
 /* quicklz/quicklz.c:777-836 -- decompress one block; returns dsize.
  * `scratch_decompress` (>= 16 B, QLZ_SCRATCH_DECOMPRESS) is accepted and unused.
- * A corrupt stream returns 0 instead of the reference's undefined behaviour. */
+ * A corrupt stream returns 0 instead of the reference's undefined behaviour
+ * (qlzx_last_status() says why).
+ * Fail-stop: the three GPU-backed drop-ins (qlz_decompress, qlz_compress,
+ * crc32_write) have no error channel in their callers (quicklz/cquicklz.go:38-40,
+ * store/crc32.go:81-84), so a runtime failure (no device, a HIP error) prints
+ * qlzx_last_error() to stderr and abort()s instead of returning a wrong value. */
 size_t qlz_decompress(const char *source, void *destination, char *scratch_decompress);
 /* quicklz/quicklz.c:692-775 -- compress one block (level 3); returns csize,
  * 0 if size == 0 or size > 0xffffffff-400.  destination >= size + 400 bytes.
@@ -127,7 +132,8 @@ size_t qlzx_compress1(const void *source, char *destination, size_t size, uint32
 
 /* ---- Go quicklz level 1 (quicklz.go:80-191 and 291-431) ----
  * One lane per block with its hash tables in `workspace` (16-B aligned,
- * qlzx_go_l1_workspace_size(n) bytes).  Production gobeansdb writes level 3 through
+ * qlzx_go_l1_workspace_size(n) bytes for compress, qlzx_go_decompress_workspace_size(n)
+ * for decompress; both bounded: launches of at most 65536 blocks reuse them).  Production gobeansdb writes level 3 through
  * cgo; these serve the Go Compress(src, 1) / Decompress surface.
  * compress:   dst capacity >= src_len + 400 per block; empty block -> QLZX_E_EMPTY
  *             (Go returns nil); output bytes = Go Compress(src, 1).
@@ -139,8 +145,14 @@ int qlzx_go_l1_compress_batch(const qlzx_blocks *b, uint32_t *csize, int32_t *st
                               size_t workspace_bytes, void *stream);
 int qlzx_go_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_t *dsize, int32_t *status,
                              void *workspace, size_t workspace_bytes, void *stream);
+/* Workspace of qlzx_go_decompress_batch (the decoder needs only the 16 KiB hashtable per
+ * block; launches cover at most 65536 blocks and reuse it). */
+size_t qlzx_go_decompress_workspace_size(uint32_t n);
 /* Single-block Go Decompress of a stored or level-1 stream of source_len bytes into
- * destination (capacity dst_cap): returns the decompressed size, 0 on error. */
+ * destination (capacity dst_cap): returns the decompressed size (0 is a valid empty
+ * result), QLZX_GO_ERROR on error; qlzx_last_status() then holds the block's
+ * enum qlzx_status (QLZX_E_CORRUPT where Go panics) and qlzx_last_error() the reason. */
+#define QLZX_GO_ERROR ((size_t)-1)
 size_t qlzx_go_decompress1(const char *source, size_t source_len, void *destination, size_t dst_cap);
 
 /* CRC32 of many buffers: out[i] = crc32_write(init ? init[i] : 0xffffffff, src_i) ^ (final_xor).
@@ -189,6 +201,10 @@ int qlzx_replay_index(const uint8_t *data, uint64_t size, uint64_t start, uint32
 /* Getvhash (store/item.go:89-100, Fnv1a of utils/hash.go:8-16) of n values. */
 int qlzx_vhash_batch(const uint8_t *src, const uint64_t *off, const uint32_t *len, uint32_t n, uint16_t *out,
                      void *stream);
+
+/* enum qlzx_status of the calling thread's last single-block call (qlz_decompress,
+ * qlzx_compress1, qlzx_go_decompress1). */
+int qlzx_last_status(void);
 
 /* Last error message of the calling thread (empty if none). */
 const char *qlzx_last_error(void);

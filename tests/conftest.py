@@ -47,12 +47,3 @@ def cuda():
     from gobeansdb_amd import build
     build.build()
     return torch.device("cuda:0")
-
-
-@pytest.fixture(params=["items", "split", "seq"])
-def k2(request, monkeypatch):
-    """Runs a decode test once per K2 kernel: k_dec_blocks (default), k_dec_split
-    (QLZX_K2=split) and k_dec_seq (QLZX_K2=seq); the library reads the variable on every
-    batch call."""
-    monkeypatch.setenv("QLZX_K2", request.param)
-    return request.param

@@ -43,3 +43,22 @@ def test_header_helpers(golden):
 
 def test_info_names_gfx950():
     assert "gfx950" in _lib.info()
+
+
+def test_drop_ins_fail_stop_without_a_device():
+    """The quicklz.h drop-ins have no error channel in their Go callers
+    (quicklz/cquicklz.go:38-40, store/crc32.go:81-84): on a host with no GPU, qlz_compress,
+    qlz_decompress and crc32_write must stop the process with the reason, not return 0 (an
+    empty "compressed" value) or the input CRC state (a plausible wrong record CRC)."""
+    import sys
+    build.build()
+    for call in ("L.qlz_compress(b'abcdefgh' * 64, ctypes.create_string_buffer(1024), 512, None)",
+                 "L.qlz_decompress(bytes([0x4d, 12, 3]) + bytes(9), ctypes.create_string_buffer(64), None)",
+                 "L.crc32_write(0xffffffff, b'abc', 3)"):
+        code = ("import ctypes, sys; sys.path.insert(0, %r); from gobeansdb_amd import _lib; "
+                "L = _lib.lib(); r = %s; print('returned', r)") % (os.path.dirname(os.path.dirname(__file__)), call)
+        env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+        p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+        assert p.returncode != 0, (call, p.stdout, p.stderr)
+        assert "returned" not in p.stdout
+        assert "libqlzx:" in p.stderr and "no error channel" in p.stderr, p.stderr

@@ -57,7 +57,7 @@ def test_compress_golden_bit_exact(cuda, golden):
 
 # general=True: every block through the general lane-per-block kernel (values over 64 KiB)
 @pytest.mark.parametrize("general", [False, True])
-def test_decompress_golden(cuda, golden, general, k2):
+def test_decompress_golden(cuda, golden, general):
     vs = golden.vectors
     outs, st, crc = _gpu_decompress([golden.get(v["c_out"]) for v in vs], want_crc=True, general=general)
     assert (st == 0).all(), [(v["name"], s) for v, s in zip(vs, st) if s]
@@ -108,7 +108,7 @@ def test_cdecompress_safe_errors(cuda, golden):
 
 
 @pytest.mark.parametrize("general", [False, True])
-def test_corrupt_status_matches_oracle(cuda, golden, general, k2):
+def test_corrupt_status_matches_oracle(cuda, golden, general):
     rng = np.random.default_rng(5)
     base = [golden.get(v["c_out"]) for v in golden.vectors if v["cls"] in ("text", "runs", "kat") and v["n"] >= 100]
     cases = []
@@ -191,7 +191,7 @@ def test_go_compat_compress(cuda):
 
 
 @pytest.mark.parametrize("general", [False, True])
-def test_record_fused_crc_verify(cuda, golden, general, k2):
+def test_record_fused_crc_verify(cuda, golden, general):
     """store/datafile.go:161-168: CRC over header[4:24] ‖ key ‖ value, fused with decompress."""
     import struct
     import torch
@@ -221,7 +221,7 @@ def test_record_fused_crc_verify(cuda, golden, general, k2):
 
 
 @pytest.mark.parametrize("crc", [False, True])
-def test_multi_chunk_overlap_round_trip(cuda, crc, k2):
+def test_multi_chunk_overlap_round_trip(cuda, crc):
     """More blocks than one decode chunk (131072): K1 of chunk c+1 runs on the side stream while K2
     of chunk c runs (two workspace halves).  Every block must round-trip, and with crc the fused
     record CRC must equal a separate CRC pass over the compressed values."""
@@ -251,7 +251,7 @@ def test_multi_chunk_overlap_round_trip(cuda, crc, k2):
         assert torch.equal(crc_out, batch.crc32(src))
 
 
-def test_mixed_sizes_block_order_round_trip(cuda, k2):
+def test_mixed_sizes_block_order_round_trip(cuda):
     """Log-uniform 1-64 KiB text and image-like blocks over two decode chunks: K1 and K2 take
     their blocks from the size-ordered list (k_order_count / k_order_scatter), so every block's
     output must still land at its own offset.  Compared by per-block CRC32 of output vs plain."""
@@ -301,3 +301,55 @@ def test_max_dsize_contract(cuda):
         for n, p, g, s in zip(sizes, plain, got, st):
             if s == 0:
                 assert g == p
+
+
+@pytest.mark.parametrize("general", [False, True])
+@pytest.mark.parametrize("with_cap", [False, True])
+def test_max_dsize_above_fast_limit(cuda, general, with_cap):
+    """max_dsize above the fast-path limit: blocks over 64 KiB take the general kernel, which
+    must also refuse a block whose dsize exceeds max_dsize (QLZX_E_MAX_DSIZE, nothing written),
+    with and without dst_cap, and with no workspace at all (general=True)."""
+    import torch
+    from gobeansdb_amd import _lib, batch
+    md = 100000
+    sizes = [200000, 90000, 16000, 100000]
+    plain = [O.gen_text(4, i, n) for i, n in enumerate(sizes)]
+    comp = [O.compress(p) for p in plain]
+    src = batch.BlockBatch.from_bytes(comp)
+    out_sizes = [min(n, md) for n in sizes]   # destinations sized by max_dsize
+    out = batch.BlockBatch.empty_for(out_sizes)
+    guard = out.data.clone()
+    cap = torch.tensor(out_sizes, dtype=torch.int32, device="cuda") if with_cap else None
+    dsz, st, _ = batch.decompress(src, out, dst_cap=cap, max_dsize=md, general=general)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy().tolist()
+    assert st == [_lib.E_MAX_DSIZE, 0, 0, 0], st
+    got = out.to_bytes(dsz.cpu().numpy())
+    for p, g, s in zip(plain, got, st):
+        if s == 0:
+            assert g == p
+    # the refused block's destination is untouched
+    o0 = int(out.off[0])
+    assert torch.equal(out.data[o0:o0 + out_sizes[0]], guard[o0:o0 + out_sizes[0]])
+
+
+def test_go_decompress1_error_channel(cuda):
+    """A compressed level-1 stream with dsize 0 whose first control word has a match bit: Go
+    panics on destination[0]; qlzx_go_decompress1 must report QLZX_GO_ERROR (not 0 == a valid
+    empty result) and the Decompress mirror must raise."""
+    import struct
+    from gobeansdb_amd import _lib
+    from gobeansdb_amd.quicklz import Decompress, QuicklzError
+    L = _lib.lib()
+    for cw, want in ((0x80000001, _lib.E_CORRUPT), (0x80000000, _lib.OK)):
+        s = bytes([0x47]) + struct.pack("<II", 17, 0) + struct.pack("<I", cw) + bytes([0, 1, 2, 3])
+        assert O.decompress_go_l1(s)[0] == want
+        dst = ctypes.create_string_buffer(1)
+        r = L.qlzx_go_decompress1(s, len(s), dst, 0)
+        if want == _lib.OK:
+            assert r == 0 and L.qlzx_last_status() == _lib.OK
+            assert Decompress(s) == b""
+        else:
+            assert r == _lib.GO_ERROR and L.qlzx_last_status() == want
+            with pytest.raises(QuicklzError):
+                Decompress(s)

@@ -34,7 +34,7 @@ def test_compress_bytes_equal_oracle(cuda, kind, n):
 
 
 @pytest.mark.parametrize("kind,n", [("text", 2048), ("mixed", 1024)])
-def test_decompress_oracle_streams(cuda, k2, kind, n):
+def test_decompress_oracle_streams(cuda, kind, n):
     import torch
     from gobeansdb_amd import batch
     rng = np.random.default_rng(7 + len(kind))

@@ -100,3 +100,29 @@ def test_go_compat_mode(n):
     g = O.compress_go(data)
     assert g[0] & 2 and int.from_bytes(g[1:5], "little") == len(g)
     assert O.decompress(g) == (O.OK, data)
+
+
+def test_go_compat_core_matches_reference_core(golden):
+    """Go Compress(src, 3) (quicklz.go:80-289, the QLZX_F_GO_COMPAT mode) against the reference
+    quicklz.c stream of every golden vector: after the header the core streams are identical,
+    except where the Go encoder differs by construction:
+      * its bail-out counts the 9-byte header (quicklz.go:119), so it may give up (stored) where
+        C still emits a compressed stream;
+      * it has no 9-byte core minimum (quicklz.c:493 pads tiny cores with destination bytes).
+    Every Go stream must still decode to the input (the KAT pins the 116-B length)."""
+    quirks = []
+    for v in golden.vectors:
+        data, c = golden.get(v["input"]), golden.get(v["c_out"])
+        go = O.compress_go(data)
+        assert go[0] & 2 and int.from_bytes(go[1:5], "little") == len(go), v["name"]
+        assert int.from_bytes(go[5:9], "little") == len(data), v["name"]
+        assert O.decompress(go) == (O.OK, data), v["name"]
+        hdr = 9 if c[0] & 2 else 3
+        if (go[0] & 1) == (c[0] & 1) and go[9:] == c[hdr:]:
+            continue
+        go_bailed = (go[0] & 1) == 0 and (c[0] & 1) == 1
+        core_min = (c[0] & 1) and len(c) - hdr == 9 and c[hdr:].startswith(go[9:]) and len(go) - 9 < 9
+        assert go_bailed or core_min, v["name"]
+        quirks.append((v["name"], "bail-out" if go_bailed else "core-min"))
+    # the quirks stay the exception
+    assert len(quirks) <= len(golden.vectors) // 4, quirks

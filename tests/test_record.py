@@ -25,6 +25,27 @@ def test_need_compress_sniff_table(data, expect):
     assert record.need_compress(value[:512]) == expect
 
 
+# the same sniffTests data under the shipped conf/global.yaml:29-33 set (adds audio/ogg and
+# audio/midi): MIDI is now stored raw; Ogg still compresses because Go 1.13 answers
+# "application/ogg" (store/item_test.go:19), never "audio/ogg".
+SNIFF_SHIPPED = [(d, e and not d.startswith(b"MThd")) for d, e in SNIFF]
+
+
+@pytest.mark.parametrize("data,expect", SNIFF_SHIPPED)
+def test_need_compress_shipped_not_compress_set(data, expect):
+    value = data + bytes(512 - len(data))
+    assert record.need_compress(value[:512], record.NOT_COMPRESS_SHIPPED) == expect
+
+
+def test_sniff_answers():
+    assert record.sniff(b"MThd\x00\x00\x00\x06" + bytes(8)) == "audio/midi"
+    assert record.sniff(b"MThd\x00\x00\x00\x07" + bytes(8)) is None        # header length must be 6
+    assert record.sniff(b"OggS\x00" + bytes(8)) == "application/ogg"
+    assert record.sniff(b"RIFF\x01\x02\x03\x04AVI " + bytes(8)) == "video/avi"
+    assert record.sniff(b".snd" + bytes(8)) == "audio/basic"
+    assert record.sniff(b"MTh") is None                                         # too short to match
+
+
 def test_riff_webp_is_not_wave():
     assert record.need_compress(b"RIFF\x00\x00\x00\x00WEBPVP8 " + bytes(100))
 
