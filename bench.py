@@ -13,7 +13,9 @@ barrier + synchronize bracketed and max-reduced over ranks.
 Prints one JSON line (rank 0).  See DESIGN.md §3 for the roofline accounting.  The default c2
 run (1 M x 16 KiB) also measures BASELINE config c3 -- compress + fused CRC32 of 1 M x 64 KiB
 image-like values, the "(+compress)" of the metric -- after releasing the c2 buffers, and reports
-it under "compress" in the same line (--no-c3 skips it; --config c3 runs it alone); then config c5
+it under "compress" in the same line (--no-c3 skips it; --config c3 runs it alone); then config c4
+-- .data replay of two distinct chunk files, device-resident and pipelined end to end -- under
+"replay" (--no-c4 skips it); then config c5
 -- 400 GiB of mixed 4-64 KiB values split over the ranks, strong scaling -- under "mixed"
 (--no-c5 skips it; --config c5 runs it alone).
 """
@@ -71,6 +73,10 @@ def parse():
     p.add_argument("--no-c5", action="store_true",
                    help="c2 run: skip the c5 leg (400 GiB of mixed values over the ranks, strong "
                         "scaling) reported under \"mixed\" in the same line")
+    p.add_argument("--no-c4", action="store_true",
+                   help="c2 run: skip the c4 .data replay leg reported under \"replay\" in the same line")
+    p.add_argument("--c4-chunk-mib", type=int, default=4000, help="c4 leg: MiB per chunk file (two distinct)")
+    p.add_argument("--c4-files", type=int, default=13, help="c4 leg: files replayed end to end (~50 GiB)")
     p.add_argument("--crc", action="store_true", help="fused record CRC verify in the timed pass")
     p.add_argument("--traffic-json", default=None,
                    help="PMC HBM bytes per block (tools/traffic.py output); default: the committed "
@@ -267,6 +273,20 @@ def main():
         a3.mode, a3.block_size, a3.steps, a3.warmup = "compress", 65536, args.c3_steps, 1
         a3.traffic_json = None
         comp = bench_compress(a3, rank, world, dev, "image", emit=False)
+    replay_rec = None
+    if not args.no_c4 and legs:
+        # BASELINE config c4: .data replay (scan + CRC + decompress + vhash), device-resident and
+        # end to end from pinned host memory, two distinct chunk files per rank
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_replay as c4mod
+        a4 = argparse.Namespace(chunk_mib=256 if args.legs_small else args.c4_chunk_mib,
+                                files=4 if args.legs_small else args.c4_files, steps=4, seed=2026,
+                                cpu_seconds=max(2.0, args.cpu_seconds / 2), no_cpu=args.no_cpu)
+        replay_rec = c4mod.run(a4, rank, world, dev)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
     mixed = None
     if not args.no_c5 and legs:
         # BASELINE config c5 in the same run: 400 GiB of mixed 4-64 KiB values split over the
@@ -282,6 +302,8 @@ def main():
         if comp is not None:
             rec["compress"] = {k: comp[k] for k in ("value", "unit", "steps", "warmup", "ms_per_step", "config",
                                                     "roofline", "cpu_baseline")}
+        if replay_rec is not None:
+            rec["replay"] = replay_rec
         if mixed is not None:
             rec["mixed"] = {k: mixed[k] for k in ("metric", "value", "unit", "scaling", "rounds_per_gpu", "wall_s",
                                                   "config", "roofline")}

@@ -855,6 +855,18 @@ __global__ void __launch_bounds__(64) k_dec_blocks(qlzx_blocks b, uint32_t *dsiz
     }
 }
 
+}  // namespace qlzx
+#include "qlzx_decode_bytes.hip"
+namespace qlzx {
+
+#ifndef QLZX_K2B_WIN
+#define QLZX_K2B_WIN 4096
+#endif
+#ifndef QLZX_K2B_MR
+#define QLZX_K2B_MR 256
+#endif
+constexpr uint32_t kWinB = QLZX_K2B_WIN, kMarkRing = QLZX_K2B_MR;
+
 inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uint32_t *dsize,
                               int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
                               uint32_t *crc_out, uint32_t max_dsize, void *ws, size_t ws_bytes,
@@ -934,8 +946,13 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
                                crc_state, crc_expect, crc_out, first, cnt, info, recs, gmax, order, max_dsize);
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
         // one kernel for every block size: the LDS window slides over longer blocks
+#ifdef QLZX_K2_ITEMS
         hipLaunchKernelGGL(k_dec_blocks<kWin>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info, recs,
                            gmax, (const uint32_t *)order);
+#else
+        hipLaunchKernelGGL((k_dec_bytes<kWinB, kMarkRing>), dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt,
+                           info, recs, gmax, (const uint32_t *)order);
+#endif
         if (overlap) (void)hipEventRecord(ev_k2[c & 1], s);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;

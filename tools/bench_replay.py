@@ -7,15 +7,17 @@ of --chunk-mib MiB is built once from synthetic values (log-uniform 4-64 KiB,
 the MIME sniff of the first 512 B (gobeansdb_amd.record.need_compress), a trial compress
 of the first 10 KiB kept when float32(clen)/float32(tlen) <= 0.7, then the whole body.
 Keys are "key_%016x".
---files copies of that chunk (13 x 4000 MiB ~ 50 GiB by default) are replayed:
+Two such chunks are built from distinct seeds; --files files alternating them (13 x 4000 MiB
+~ 50 GiB by default) are replayed:
 
   device-only   the chunk is resident in HBM; one step = qlzx_replay_index +
                 decompress of FLAG_COMPRESS values + Getvhash (gobeansdb_amd.replay)
-  end-to-end    per file: pinned H2D of the chunk, the same replay, D2H of the
-                values (decompressed or raw) into pinned host memory
+  end-to-end    pipelined per file: pinned H2D of the chunk, the same replay, D2H of
+                the decompressed values into pinned host memory, three streams
 
-Prints one JSON line.  The reference's sequential DataStreamReader is the CPU
-baseline for this path only in DESIGN.md prose (it is not shipped to the box).
+The CPU leg runs the reference record loop (crc32_write + qlz_decompress + Getvhash from
+oracle/_ref) over the first chunk.  bench.py runs this as its "replay" leg (run()); run
+alone it prints one JSON line.
 """
 from __future__ import annotations
 
@@ -116,70 +118,96 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--chunk-mib", type=int, default=4000)
     p.add_argument("--files", type=int, default=13)
-    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--steps", type=int, default=4)
     p.add_argument("--seed", type=int, default=2026)
     p.add_argument("--cpu-seconds", type=float, default=8.0)
     p.add_argument("--no-cpu", action="store_true")
     a = p.parse_args()
-    from gobeansdb_amd import replay, batch
-    dev = torch.device("cuda", 0)
+    rec = run(a, 0, 1, torch.device("cuda", 0))
+    print(json.dumps(rec), flush=True)
+
+
+HBM_PEAK_GBS = 8000.0
+
+
+def run(a, rank: int, world: int, dev):
+    """c4 on this rank: two distinct chunk files (seeds a.seed + 2 rank and + 1), each built,
+    replayed once against its expected record set, then timed device-only (steps alternate the
+    two resident chunks) and end to end from pinned host memory (a.files files alternating the
+    two chunks, so consecutive files are different bytes).  Returns the rank's record (rank 0:
+    max-over-ranks times and summed bytes; the CPU leg at N = 1 only)."""
+    from gobeansdb_amd import replay, batch, shard
     t0 = time.time()
-    host, nrec, stored_bytes, raw_bytes, rec_off = build_chunk(a.chunk_mib, a.seed, dev)
-    log(f"chunk built in {time.time() - t0:.1f}s: {len(host) / 2**20:.0f} MiB, {nrec} records")
-    pinned = torch.from_numpy(host).pin_memory()
-    dchunk = pinned.to(dev, non_blocking=False)
+    chunks = []
+    for j in range(2):
+        host, nrec, stored_bytes, raw_bytes, rec_off = build_chunk(a.chunk_mib, a.seed + 2 * rank + j, dev)
+        chunks.append(dict(host=host, nrec=nrec, raw=raw_bytes, rec_off=rec_off,
+                           pinned=torch.from_numpy(host).pin_memory()))
+    log(f"rank {rank}: two chunks built in {time.time() - t0:.1f}s: "
+        f"{[len(c['host']) >> 20 for c in chunks]} MiB, {[c['nrec'] for c in chunks]} records")
     ws = batch.Workspace(dev)
-    # correctness gate: every record found, no resync, values decompressed to their raw sizes
-    res = replay.replay(dchunk, workspace=ws)
-    torch.cuda.synchronize()
-    assert res.n == nrec and not res.end_error, (res.n, nrec, res.end_error)
-    assert int(res.size_broken.abs().sum()) == 0
-    assert int(res.value_len.to(torch.int64).sum()) == raw_bytes, "decompressed sizes"
-    assert int(((res.flag & 0x10000) != 0).sum()) == 0, "a compressed value failed to decode"
-    log("replay verified: all records, all values decoded")
+    for c in chunks:
+        c["dev"] = c["pinned"].to(dev, non_blocking=False)
+        # correctness gate: every record found, no resync, values decompressed to their raw sizes
+        res = replay.replay(c["dev"], workspace=ws)
+        torch.cuda.synchronize()
+        assert res.n == c["nrec"] and not res.end_error, (res.n, c["nrec"], res.end_error)
+        assert int(res.size_broken.abs().sum()) == 0
+        assert int(res.value_len.to(torch.int64).sum()) == c["raw"], "decompressed sizes"
+        assert int(((res.flag & 0x10000) != 0).sum()) == 0, "a compressed value failed to decode"
+        c["compressed"] = int(((res.header[:, 2] & 0x10000) != 0).sum())
+        c["out_cap"] = res.values.data.numel()
+        del res
+    log("replay verified: all records, all values decoded, both chunks")
+    stream = torch.cuda.current_stream(dev)
 
-    # ---- device-only ----
-    for _ in range(1):
-        replay.replay(dchunk, workspace=ws)
-    torch.cuda.synchronize()
+    def sync_all():
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    # ---- device-only: the chunk resident in HBM ----
+    replay.replay(chunks[0]["dev"], workspace=ws)
+    sync_all()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t = time.perf_counter()
-    for _ in range(a.steps):
-        replay.replay(dchunk, workspace=ws)
-    torch.cuda.synchronize()
-    dev_s = (time.perf_counter() - t) / a.steps
+    e0.record(stream)
+    for k in range(a.steps):
+        replay.replay(chunks[k & 1]["dev"], workspace=ws, stream=stream)
+    e1.record(stream)
+    sync_all()
+    dev_wall = time.perf_counter() - t
+    dev_ev = e0.elapsed_time(e1) * 1e-3
+    chunk_b = [len(c["host"]) for c in chunks]
+    steps_chunk = sum(chunk_b[k & 1] for k in range(a.steps))
+    steps_out = sum(chunks[k & 1]["raw"] for k in range(a.steps))
 
-    # ---- end-to-end: H2D chunk, replay, D2H values ----
-    # only decompressed values travel back: raw values are bytes the host already holds (its own file)
-    out_host = torch.empty(max(res.values.data.numel(), 1), dtype=torch.uint8).pin_memory()
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(a.files):
-        dchunk.copy_(pinned, non_blocking=True)
-        r = replay.replay(dchunk, workspace=ws)
-        out_host[: r.values.data.numel()].copy_(r.values.data, non_blocking=True)
-    torch.cuda.synchronize()
-    e2e_s = time.perf_counter() - t
-
-    # ---- end-to-end, pipelined: H2D of file i+1 || replay of file i || D2H of file i-1 ----
-    # three streams, two device chunk slots and two pinned output slots (PCIe is full duplex)
+    # ---- end to end, pipelined: H2D of file i+1 || replay of file i || D2H of file i-1 ----
+    # three streams, two device chunk slots and two pinned output slots (PCIe is full duplex);
+    # only decompressed values travel back (raw values are bytes the host already holds)
+    cap = max(c["out_cap"] for c in chunks)
     s_h2d, s_cmp, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    dslot = [dchunk, torch.empty_like(dchunk)]
-    hslot = [out_host, torch.empty_like(out_host).pin_memory()]
+    dslot = [chunks[0]["dev"], chunks[1]["dev"]]
+    hslot = [torch.empty(cap, dtype=torch.uint8).pin_memory() for _ in range(2)]
     ev_in = [torch.cuda.Event(), torch.cuda.Event()]      # chunk landed in slot
     ev_used = [torch.cuda.Event(), torch.cuda.Event()]    # replay done with slot
     ev_out = [torch.cuda.Event(), torch.cuda.Event()]     # D2H done with host slot
-    torch.cuda.synchronize()
+    sync_all()
     t = time.perf_counter()
     with torch.cuda.stream(s_h2d):
-        dslot[0].copy_(pinned, non_blocking=True)
+        dslot[0][: chunk_b[0]].copy_(chunks[0]["pinned"], non_blocking=True)
         ev_in[0].record(s_h2d)
+    e2e_bytes = 0
     for i in range(a.files):
         k = i & 1
-        if i + 1 < a.files:   # prefetch the next file while this one replays
+        n_i = chunk_b[k]
+        e2e_bytes += n_i
+        if i + 1 < a.files:   # prefetch the next file (the other chunk) while this one replays
             with torch.cuda.stream(s_h2d):
                 if i >= 1:
                     s_h2d.wait_event(ev_used[k ^ 1])
-                dslot[k ^ 1].copy_(pinned, non_blocking=True)
+                dslot[k ^ 1].copy_(chunks[k ^ 1]["pinned"], non_blocking=True)
                 ev_in[k ^ 1].record(s_h2d)
         with torch.cuda.stream(s_cmp):
             s_cmp.wait_event(ev_in[k])
@@ -193,29 +221,39 @@ def main():
             hslot[k][:nb].copy_(r.values.data, non_blocking=True)
             r.values.data.record_stream(s_d2h)
             ev_out[k].record(s_d2h)
-    torch.cuda.synchronize()
+    sync_all()
     pipe_s = time.perf_counter() - t
-    chunk_gib = len(host) / 2**30
-    cpu = None if a.no_cpu else cpu_baseline(host, rec_off, a.cpu_seconds)
-    rec = {
+    dev_wall, dev_ev, pipe_s = shard.max_over_ranks([dev_wall, dev_ev, pipe_s], device=dev)
+    tot = shard.sum_over_ranks({"chunk": steps_chunk, "out": steps_out, "e2e": e2e_bytes}, device=dev)
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(chunks[0]["host"], chunks[0]["rec_off"], a.cpu_seconds)
+    if rank != 0:
+        return None
+    achieved = (tot["chunk"] + tot["out"]) / world / a.steps / (dev_ev / a.steps) / 1e9
+    return {
         "metric": "GiB/s .data replay (record scan + CRC + decompress + vhash), c4",
-        "chunk_mib": a.chunk_mib, "records_per_chunk": nrec,
-        "compressed_values": int(((res.header[:, 2] & 0x10000) != 0).sum()),
-        "device_only": {"gib_per_s_chunk": round(chunk_gib / dev_s, 2),
-                        "gib_per_s_values_out": round(raw_bytes / 2**30 / dev_s, 2),
-                        "ms_per_chunk": round(dev_s * 1e3, 2)},
-        "end_to_end": {"files": a.files, "total_gib": round(chunk_gib * a.files, 2),
-                       "gib_per_s_chunk": round(chunk_gib * a.files / e2e_s, 2),
-                       "seconds": round(e2e_s, 2),
-                       "note": "sequential per file: pinned H2D of the chunk, replay, pinned D2H of the decompressed values"},
-        "end_to_end_pipelined": {"files": a.files, "gib_per_s_chunk": round(chunk_gib * a.files / pipe_s, 2),
+        "value": round(tot["chunk"] / dev_wall / 2**30, 2), "unit": "GiB/s of chunk, device-resident",
+        "ms_per_step": round(dev_wall * 1e3 / a.steps, 3), "steps": a.steps,
+        "config": {"workload": f"c4: two distinct {a.chunk_mib} MiB .data chunk files per GPU "
+                               "(store/datafile.go layout, log-uniform 4-64 KiB values, 70 % text, TryCompress "
+                               "policy), replayed as buildHintFromData reads them (store/bucket.go:89-117)",
+                   "records_per_chunk": [c["nrec"] for c in chunks],
+                   "compressed_values": [c["compressed"] for c in chunks],
+                   "chunk_bytes": chunk_b, "parallelism": f"shard{world}"},
+        "values_out_gib_per_s": round(tot["out"] / dev_wall / 2**30, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "what": "per step: every chunk byte read once (scan + CRC) + every value byte written",
+                     "kernel_ms": round(dev_ev * 1e3 / a.steps, 3)},
+        "end_to_end_pipelined": {"files": a.files, "total_gib": round(tot["e2e"] / 2**30, 2),
+                                 "gib_per_s_chunk": round(tot["e2e"] / pipe_s / 2**30, 2),
                                  "seconds": round(pipe_s, 2),
-                                 "note": "H2D of file i+1, replay of file i and D2H of file i-1 on three streams, "
-                                         "two device chunk slots, two pinned output slots"},
+                                 "note": "files alternate the two chunks; pinned H2D of file i+1, replay of file i "
+                                         "and pinned D2H of file i-1's decompressed values on three streams"},
         "data": "synthetic",
         "cpu_baseline": cpu,
     }
-    print(json.dumps(rec), flush=True)
 
 
 def cpu_baseline(host: np.ndarray, rec_off: np.ndarray, seconds: float):
