@@ -37,27 +37,6 @@ constexpr uint32_t kChunk = 256;        // output bytes per chunk phase (4 per l
 constexpr uint16_t kMkLit = 1;          // marker of a literal (match offsets are >= 3, check C3)
 constexpr uint16_t kSpLit = 0xFFFFu;    // pointer-array entry of a literal byte (no source)
 
-// Prefetch loads as inline asm: the compiler does not track them, so its own vmcnt waits
-// (far loads) never wait for them, and the kernel waits for them exactly where it needs them
-// (k2b_wait).  A later wait can only be stricter for them: vmcnt retires in issue order.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint32_t k2b_ld32(const void *p) {
-    uint32_t v;
-    asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-__device__ __forceinline__ u32x4 k2b_ld128(const void *p) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-// Wait until at most N vector-memory operations are outstanding; the registers are operands so
-// nothing that reads them is scheduled above the wait.
-template <int N>
-__device__ __forceinline__ void k2b_wait(uint32_t &t, u32x4 &g) {
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(t), "+v"(g) : "n"(N) : "memory");
-}
-
 template <uint32_t W, uint32_t MR>
 struct K2bLds {
     uint8_t win[W];
@@ -120,29 +99,24 @@ __global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize
     const uint32_t tail_from = dsize > QLZX_TAIL ? dsize - 1 - QLZX_TAIL : 0;  // op >= this: tail (quicklz.c:503)
 
     // ---- prefetch pipeline: the GroupRec of batch bt+1 and the token dword of batch bt are in
-    // registers (issued while batch bt-1 was decoded)
+    // registers (loaded while batch bt-1 was decoded; plain loads, so the compiler waits for them)
     ItemCursor c1{lane / 31, lane % 31};  // item coordinates of batch bt+1 once the prologue ran
-    auto rec_ptr = [&](const ItemCursor &c, bool v) -> const void * { return rb + (v ? c.g : 0u); };
-    auto tok_pos = [&](const u32x4 &gr, const ItemCursor &c, bool v, uint32_t &p) -> uint32_t {
-        // gr = {ip, m, a, b}
+    auto load_rec = [&](const ItemCursor &c, bool v) -> GroupRec { return rb[v ? c.g : 0u]; };
+    auto tok_pos = [&](const GroupRec &gr, const ItemCursor &c, bool v, uint32_t &p) -> uint32_t {
         const uint32_t low = (1u << c.k) - 1u;
-        const uint32_t pos = gr.x + 4 + c.k + __builtin_popcount(gr.z & low) + 2 * __builtin_popcount(gr.w & low);
+        const uint32_t pos = gr.ip + 4 + c.k + __builtin_popcount(gr.a & low) + 2 * __builtin_popcount(gr.b & low);
         p = v ? (pos + 4 <= csize ? pos : csize - 4) : 0u;
-        return v ? (pos | (((gr.y >> c.k) & 1u) << 31)) : 0u;
+        return v ? (pos | (((gr.m >> c.k) & 1u) << 31)) : 0u;
     };
     uint32_t posm0, tok0, tp;
-    u32x4 gr1;
     {
         const bool v0 = lane < nitems;
-        u32x4 g0 = k2b_ld128(rec_ptr(c1, v0));
-        uint32_t dummy = 0;
-        k2b_wait<0>(dummy, g0);
+        const GroupRec g0 = load_rec(c1, v0);
         posm0 = tok_pos(g0, c1, v0, tp);
-        tok0 = k2b_ld32(src + tp);  // unaligned dword (unaligned access mode)
+        tok0 = *(const uint32_t *)(src + tp);  // unaligned dword (unaligned access mode)
     }
     c1.next();
-    gr1 = k2b_ld128(rec_ptr(c1, 64 + lane < nitems));
-    bool stored_last = false;  // the newest vector-memory operation is a chunk store
+    GroupRec gr1 = load_rec(c1, 64 + lane < nitems);
     PROF_DECL
     uint32_t D = 0;          // output start of the next batch's first item
     uint32_t bt = 0;         // next batch to decode
@@ -156,17 +130,13 @@ __global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize
             if (pend == 0) {
                 if (complete || D >= c + kChunk) break;
                 if (bt >= nb) { err = true; break; }  // stream ended before dsize (check C5)
-                // gr1 and tok0 (issued one batch ago) have landed; a chunk store may be newer
-                if (stored_last) k2b_wait<1>(tok0, gr1);
-                else k2b_wait<0>(tok0, gr1);
                 const bool v = bt * 64 + lane < nitems;
                 // prefetch: token of batch bt+1 (its GroupRec is in gr1), GroupRec of batch bt+2
                 const bool v1 = (bt + 1) * 64 + lane < nitems;
                 const uint32_t posm1 = tok_pos(gr1, c1, v1, tp);
-                const uint32_t tok1 = k2b_ld32(src + tp);
+                const uint32_t tok1 = *(const uint32_t *)(src + tp);
                 c1.next();
-                gr1 = k2b_ld128(rec_ptr(c1, (bt + 2) * 64 + lane < nitems));
-                stored_last = false;
+                gr1 = load_rec(c1, (bt + 2) * 64 + lane < nitems);
                 // decode batch bt
                 const bool ism = (posm0 >> 31) != 0;
                 const uint32_t pos = posm0 & 0x7fffffffu;
@@ -276,7 +246,6 @@ __global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize
         } else {
             for (uint32_t j = 0; j < 4 && p0 + j < dsize; j++) dst[p0 + j] = (uint8_t)(w >> (8 * j));
         }
-        stored_last = true;
         PROF_MARK(4);  // 4: store
     }
     vm_sync();

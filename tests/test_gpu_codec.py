@@ -323,7 +323,8 @@ def test_max_dsize_above_fast_limit(cuda, general, with_cap):
     dsz, st, _ = batch.decompress(src, out, dst_cap=cap, max_dsize=md, general=general)
     torch.cuda.synchronize()
     st = st.cpu().numpy().tolist()
-    assert st == [_lib.E_MAX_DSIZE, 0, 0, 0], st
+    # with dst_cap the capacity check comes first (K1's order: cquicklz.go:45 sizes by dsize)
+    assert st == [_lib.E_DST_CAP if with_cap else _lib.E_MAX_DSIZE, 0, 0, 0], st
     got = out.to_bytes(dsz.cpu().numpy())
     for p, g, s in zip(plain, got, st):
         if s == 0:

@@ -1,0 +1,196 @@
+"""CPU model of the byte-parallel K2 (csrc/qlzx_decode_bytes.hip), lane-vectorised with numpy.
+
+A development aid: it runs the kernel's algorithm (item phase, marker ring, chunk phase with
+the marker fill, pointer jumping and window/far gather) on a stream's group records as K1
+emits them, so the design can be checked on CPU against the oracle's output.
+
+usage: python tools/k2b_model.py [W] [MR]
+"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle import oracle as O  # noqa: E402
+
+TAIL = 10
+
+
+def k1_groups(c: bytes):
+    """GroupRecs (ip, m, a, b) and nitems as k_dec_parse emits them for a valid stream."""
+    hdr = 9 if c[0] & 2 else 3
+    dsize = int.from_bytes(c[5:9], "little") if hdr == 9 else c[2]
+    ip, recs, n, op = hdr, [], 0, 0
+    csize = len(c)
+    while ip + 4 <= csize and op < dsize:
+        cw = int.from_bytes(c[ip:ip + 4], "little")
+        gip = ip
+        ip += 4
+        m = a = b = 0
+        k = 0
+        while k < 31 and ip < csize:
+            if (cw >> k) & 1:
+                t = c[ip]
+                tl = 1 if t & 3 == 0 else (2 if t & 3 != 3 else (3 if t & 127 != 3 else 4))
+                m |= 1 << k
+                if (tl - 1) & 1:
+                    a |= 1 << k
+                if (tl - 1) & 2:
+                    b |= 1 << k
+                ip += tl
+            else:
+                ip += 1
+            k += 1
+            n += 1
+        recs.append((gip, m, a, b))
+        op = dsize if ip >= csize else op   # parse to the end of the stream, like K1
+    return recs, n, dsize, hdr
+
+
+def decode_tok(t):
+    ty = (t & 3) + ((t & 127) == 3)
+    if ty == 0:
+        return (t & 0xff) >> 2, 3, 1
+    if ty == 1:
+        return (t & 0xffff) >> 2, 3, 2
+    if ty == 2:
+        return (t & 0xffff) >> 6, ((t >> 2) & 15) + 3, 2
+    if ty == 3:
+        return (t >> 7) & 0x1ffff, ((t >> 2) & 0x1f) + 2, 3
+    return t >> 15, ((t >> 7) & 255) + 3, 4
+
+
+def model(c: bytes, W=4096, MR=256):
+    recs, nitems, dsize, hdr = k1_groups(c)
+    csize = len(c)
+    cp = c + bytes(8)
+    nb = (nitems + 63) // 64
+    tail_from = dsize - 1 - TAIL if dsize > TAIL else 0
+    win = np.zeros(W, np.uint8)
+    mk = np.zeros(MR, np.int64)
+    out = np.zeros(dsize + 8, np.uint8)   # the block's destination in HBM
+    D, bt, tail, complete = 0, 0, False, dsize == 0
+    pend = np.zeros(64, bool)
+    pd = np.zeros(64, np.int64)
+    pmk = np.zeros(64, np.int64)
+    plit = np.zeros(64, np.int64)
+    cin = 0
+    c0 = 0
+    while c0 < dsize:
+        while True:
+            if not pend.any():
+                if complete or D >= c0 + 256:
+                    break
+                if bt >= nb:
+                    return "E_CORRUPT(items ran out)", None
+                lens = np.zeros(64, np.int64)
+                ism = np.zeros(64, bool)
+                offs = np.zeros(64, np.int64)
+                tls = np.zeros(64, np.int64)
+                lits = np.zeros(64, np.int64)
+                pos = np.zeros(64, np.int64)
+                valid = np.zeros(64, bool)
+                for lane in range(64):
+                    I = bt * 64 + lane
+                    if I >= nitems:
+                        continue
+                    valid[lane] = True
+                    g, k = divmod(I, 31)
+                    ip, m, a, b = recs[g]
+                    low = (1 << k) - 1
+                    p = ip + 4 + k + bin(a & low).count("1") + 2 * bin(b & low).count("1")
+                    pos[lane] = p
+                    t = int.from_bytes(cp[p:p + 4], "little")
+                    lits[lane] = t & 0xff
+                    if (m >> k) & 1:
+                        ism[lane] = True
+                        offs[lane], lens[lane], tls[lane] = decode_tok(t)
+                    else:
+                        lens[lane], tls[lane] = 1, 1
+                incl = np.cumsum(lens)
+                total = int(incl[-1])
+                d = D + incl - lens
+                live = valid & (d < dsize)
+                bad = np.zeros(64, bool)
+                last = np.zeros(64, bool)
+                if tail or D + total > tail_from:
+                    tl_lanes = np.nonzero(live & ~ism & (d >= tail_from))[0]
+                    tail_lane = 0 if tail else (int(tl_lanes[0]) if len(tl_lanes) else 64)
+                    tail = tail or len(tl_lanes) > 0
+                    lane_ix = np.arange(64)
+                    mok = (offs >= 3) & (offs <= d) & (d + lens + 4 <= dsize) & (lane_ix < tail_lane)
+                    last = live & (d + lens == dsize)
+                    ip_end = pos + tls
+                    eok = (ip_end == csize) | ((ip_end < hdr + 9) & (csize == hdr + 9))
+                    bad = live & ((ism & ~mok) | (last & ~eok))
+                else:
+                    bad = ism & ((offs < 3) | (offs > d))
+                if bad.any():
+                    return "E_CORRUPT(check)", None
+                complete = bool(last.any())
+                pend = live.copy()
+                pd = d.copy()
+                pmk = np.where(ism, offs, 1)
+                plit = lits.copy()
+                D += total
+                bt += 1
+            wr = pend & (pd < c0 + MR)
+            for lane in np.nonzero(wr)[0]:
+                mk[pd[lane] & (MR - 1)] = pmk[lane]
+                if pmk[lane] == 1:
+                    win[pd[lane] & (W - 1)] = plit[lane]
+            pend &= ~wr
+            if pend.any():
+                break
+        # chunk phase
+        p = c0 + np.arange(256)
+        m = mk[(c0 & (MR - 1)) + np.arange(256)].copy()
+        mk[(c0 & (MR - 1)) + np.arange(256)] = 0
+        f = np.zeros(256, np.int64)
+        cur = cin
+        for j in range(256):
+            cur = m[j] if m[j] else cur
+            f[j] = cur
+        cin = cur
+        s = np.where(f == 1, p, p - f)
+        q = (f != 1) & (s >= c0)
+        sp = np.where(f == 1, 0xFFFF, s & 0xFFFF)
+        while q.any():
+            t = np.where(q, sp[np.clip(s - c0, 0, 255)], 0)
+            lit = q & (t == 0xFFFF)
+            nq = q & ~lit & (t >= c0)
+            s = np.where(q & ~lit, t, s)
+            q = nq
+            sp = np.where(f == 1, 0xFFFF, s & 0xFFFF)
+        lo = c0 + MR - W if c0 + MR > W else 0
+        v = win[s & (W - 1)].copy()
+        far = s < lo
+        v[far] = out[s[far]]
+        win[p & (W - 1)] = v
+        n = min(256, dsize - c0)
+        out[c0:c0 + n] = v[:n]
+        c0 += 256
+    return "OK", bytes(out[:dsize])
+
+
+def main():
+    W = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    MR = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+    from test_gpu_decode_bytes import _cases
+    bad = 0
+    for k, x in enumerate(_cases()):
+        c = O.compress(x)
+        if not c[0] & 1:
+            continue
+        st, y = model(c, W, MR)
+        ok = st == "OK" and y == x
+        bad += not ok
+        if not ok:
+            print(k, len(x), st, None if y is None else next(i for i in range(len(x)) if y[i] != x[i]))
+    print("failures:", bad)
+
+
+if __name__ == "__main__":
+    main()
