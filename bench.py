@@ -78,6 +78,8 @@ def parse():
     p.add_argument("--c4-chunk-mib", type=int, default=4000, help="c4 leg: MiB per chunk file (two distinct)")
     p.add_argument("--c4-files", type=int, default=13, help="c4 leg: files replayed end to end (~50 GiB)")
     p.add_argument("--crc", action="store_true", help="fused record CRC verify in the timed pass")
+    p.add_argument("--no-crc-leg", action="store_true",
+                   help="skip the \"crc\" leg (the c2 shard again with the fused CRC verify)")
     p.add_argument("--traffic-json", default=None,
                    help="PMC HBM bytes per block (tools/traffic.py output); default: the committed "
                         "profiles/r02b_c2_traffic.json for the c2 workload")
@@ -218,6 +220,36 @@ def main():
     tot = shard.sum_over_ranks({"out_bytes": dsum, "in_bytes": csum}, device=dev)
     ms_per_step = wall * 1e3 / args.steps
 
+    crc_leg = None
+    if not args.crc and not args.no_crc_leg:
+        # the read path always verifies the record CRC (store/datafile.go:161-168): the same shard
+        # decoded with the CRC fused into the pass and checked against the stored values' CRCs
+        cst = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        cexp = batch.crc32(src)
+        _, st3, _ = batch.decompress(src, out, crc_state=cst, crc_expect=cexp, max_dsize=bs, workspace=ws)
+        torch.cuda.synchronize()
+        assert int((st3 != 0).sum().item()) == 0, "fused CRC verify failed"
+        for _ in range(args.warmup):
+            batch.decompress(src, out, crc_state=cst, crc_expect=cexp, max_dsize=bs, workspace=ws, stream=stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0c = time.perf_counter()
+        for _ in range(args.steps):
+            batch.decompress(src, out, crc_state=cst, crc_expect=cexp, max_dsize=bs, workspace=ws, stream=stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        wall_c = shard.max_over_ranks([time.perf_counter() - t0c], device=dev)[0]
+        crc_leg = {"value": round(tot["out_bytes"] * args.steps / wall_c / 2**30, 3), "unit": "GiB/s",
+                   "ms_per_step": round(wall_c * 1e3 / args.steps, 4),
+                   "vs_value": round((tot["out_bytes"] * args.steps / wall_c) / (tot["out_bytes"] * args.steps / wall), 4),
+                   "what": "the c2 shard decoded with the record CRC32 fused into K1 and verified against "
+                           "crc_expect per block (read path of store/datafile.go:161-168)"}
+        del cst, cexp
+
     total_out = tot["out_bytes"] * args.steps
     value = total_out / wall / 2**30
     achieved = (csum + dsum) / (kern_ms * 1e-3) / 1e9
@@ -261,6 +293,8 @@ def main():
                          "algorithmic_bytes_per_launch": csum + dsum},
             "cpu_baseline": cpu,
         }
+        if crc_leg is not None:
+            rec["crc"] = crc_leg
     comp = None
     legs = args.mode == "decompress" and args.block_size == 16384 and (args.blocks == 1 << 20 or args.legs_small)
     if not args.no_c3 and legs:

@@ -174,6 +174,9 @@ __global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize
                 posm0 = posm1;
                 tok0 = tok1;
                 bt++;
+#ifdef QLZX_PROFILE
+                _pacc[5] += 1;  // batches decoded
+#endif
             }
             // markers (and literal bytes) of the held items that start below c + MR
             const bool wr = ((pend >> lane) & 1u) && pd < c + MR;
@@ -183,6 +186,9 @@ __global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize
                 if ((pmk & 0xffffu) == kMkLit) L.win[pd & (W - 1)] = (uint8_t)(pmk >> 16);
             }
             pend &= ~wm;
+#ifdef QLZX_PROFILE
+            _pacc[6] += 1;  // marker passes
+#endif
             if (pend) break;  // the rest start at or above c + MR >= c + kChunk
         }
         if (err) break;
@@ -215,16 +221,21 @@ __global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize
             auto ent = [](uint32_t f, uint32_t s) -> uint32_t { return f == kMkLit ? (uint32_t)kSpLit : s & 0xffffu; };
             *(uint2 *)spl = make_uint2(ent(f0, s0) | (ent(f1, s1) << 16), ent(f2, s2) | (ent(f3, s3) << 16));
             do {
-                // a byte whose source reached a literal keeps it; else it takes its source's source
-                auto jump = [&](bool &q, uint32_t &s) {
-                    if (q) {
-                        const uint32_t t = L.sp[s - c];
-                        q = t != kSpLit && t >= c;
-                        s = t == kSpLit ? s : t;
-                    }
+                // a byte whose source reached a literal keeps it; else it takes its source's source.
+                // All four reads go out before any is used (one LDS round trip per round); a byte
+                // that is not jumping reads its own entry.
+                const uint32_t t0 = L.sp[(q0 ? s0 : p0) - c], t1 = L.sp[(q1 ? s1 : p0 + 1) - c];
+                const uint32_t t2 = L.sp[(q2 ? s2 : p0 + 2) - c], t3 = L.sp[(q3 ? s3 : p0 + 3) - c];
+                auto jump = [&](bool &q, uint32_t &s, uint32_t t) {
+                    const bool lit = t == kSpLit;
+                    s = q && !lit ? t : s;
+                    q = q && !lit && t >= c;
                 };
-                jump(q0, s0), jump(q1, s1), jump(q2, s2), jump(q3, s3);
+                jump(q0, s0, t0), jump(q1, s1, t1), jump(q2, s2, t2), jump(q3, s3, t3);
                 *(uint2 *)spl = make_uint2(ent(f0, s0) | (ent(f1, s1) << 16), ent(f2, s2) | (ent(f3, s3) << 16));
+#ifdef QLZX_PROFILE
+                _pacc[7] += 1;  // pointer-jumping rounds
+#endif
             } while (__ballot(q0 || q1 || q2 || q3));
         }
         PROF_MARK(2);  // 2: pointer jumping

@@ -273,19 +273,29 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
 #endif
         PROF_MARK(1);  // 1: waiting for the round's DMA
         const bool act = stream && r <= last_round;
-        if (CRC && act) {  // CRC of this round's bytes, in stream order
+        // CRC of this round's bytes [cq, chi), in stream order.  It is interleaved with the parse
+        // steps below (one 8-byte slicing step per parse iteration) and finished after them: the
+        // parse is a serial chain per lane, and the CRC steps fill its dependency bubbles instead
+        // of running ahead of it on the critical path.
+        uint32_t cq = 0, chi = 0;
+        if (CRC && act) {
             const uint32_t q0 = r * kRoundBytes, q1 = q0 + kRoundBytes;
-            const uint32_t lo = q0 > shift ? q0 : shift, hi = (q1 < span + shift) ? q1 : span + shift;
-            uint32_t q = lo;
-            while (q < hi && (q & 7u)) { crc = crc_byte(tab, crc, ring[ring_off(q, lane)]); q++; }
-            while (q + 8 <= hi) {
-                const uint32_t w0 = *(const uint32_t *)(ring + ring_off(q, lane));
-                const uint32_t w1 = *(const uint32_t *)(ring + ring_off(q + 4, lane));
-                crc = crc_slice8(tab, crc, w0, w1);
-                q += 8;
-            }
-            while (q < hi) { crc = crc_byte(tab, crc, ring[ring_off(q, lane)]); q++; }
+            cq = q0 > shift ? q0 : shift;
+            chi = (q1 < span + shift) ? q1 : span + shift;
         }
+        auto crc_step = [&]() {
+            if (cq < chi) {
+                if (!(cq & 7u) && cq + 8 <= chi) {
+                    const uint32_t w0 = *(const uint32_t *)(ring + ring_off(cq, lane));
+                    const uint32_t w1 = *(const uint32_t *)(ring + ring_off(cq + 4, lane));
+                    crc = crc_slice8(tab, crc, w0, w1);
+                    cq += 8;
+                } else {
+                    crc = crc_byte(tab, crc, ring[ring_off(cq, lane)]);
+                    cq++;
+                }
+            }
+        };
         PROF_MARK(2);  // 2: CRC
         // parse while the bytes the next step reads have landed (stream pos < lim)
         const uint32_t lim = (r + 1) * kRoundBytes - shift;
@@ -295,6 +305,7 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
             _pacc[5] += 1;
             if (go) _pacc[6] += 1;
 #endif
+            if (CRC) crc_step();
             // one step = a control word (k == 31), or a literal run (possibly empty)
             // followed by the match that ends it.  Straight-line selects; only the
             // record store branches.
@@ -339,6 +350,8 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
             done_parse = done_parse | (go & (end | bad));
             go = adv;
         }
+        if (CRC)
+            while (__ballot(cq < chi)) crc_step();  // the rest of the round's CRC
         PROF_MARK(3);  // 3: parse
         if (!CRC && done_parse) stream = false;  // nothing left to read for this lane
         // round r+3 reuses the slot of round r-1 (consumed: round r+1 reads only rounds r, r+1)

@@ -1,7 +1,8 @@
 """GPU parity at the BASELINE block shapes against the oracle (pinned to the reference
 quicklz.c by tests/golden): c2-shaped 16 KiB text blocks, c3-shaped 64 KiB image-like blocks
 and c5-shaped mixed 4-64 KiB values, a few thousand each.  Compressed bytes must equal the
-oracle's; decompressing the oracle's streams (every K2 kernel) must give the inputs back."""
+oracle's; decompressing the oracle's streams must give the inputs back, also with the fused
+record-CRC verify of the read path (store/datafile.go:161-168)."""
 import numpy as np
 import pytest
 
@@ -46,3 +47,44 @@ def test_decompress_oracle_streams(cuda, kind, n):
     torch.cuda.synchronize()
     assert st.cpu().numpy().tolist() == [0] * n
     assert out.to_bytes(dsz.cpu().numpy()) == plains
+
+
+def test_decompress_c2_shape_with_record_crc_verify(cuda):
+    """c2 shape (2,048 x 16 KiB text) through the fused CRC verify: every record CRC
+    ~crc32_write(state(header[4:24] | key), value) equals the oracle's, a flipped value byte
+    gives QLZX_E_CRC for exactly that record, and the others decode."""
+    import struct
+    import torch
+    from gobeansdb_amd import _lib, batch
+    n = 2048
+    plains = [O.gen_text(321, 40000 + i, 16384) for i in range(n)]
+    comps = [O.compress(p) for p in plains]
+    bad = {5, 777, 2047}
+    for j in bad:
+        b = bytearray(comps[j])
+        b[len(b) // 3] ^= 0x21
+        comps[j] = bytes(b)
+    states, expect = [], []
+    for i, c in enumerate(comps):
+        hdr20 = struct.pack("<IIiII", 1700000000 + i, 0x10000, 1, 20, len(c))
+        key = b"key_%016x" % i
+        st = O.crc32_write(O.crc32_write(0xFFFFFFFF, hdr20), key)
+        states.append(st)
+        good = O.compress(plains[i])   # the record was written with the good value
+        expect.append(O.crc32_write(st, good) ^ 0xFFFFFFFF)
+    src = batch.BlockBatch.from_bytes(comps)
+    out = batch.BlockBatch.empty_for([16384] * n)
+    s_t = torch.tensor(np.asarray(states, np.uint32).view(np.int32), device="cuda")
+    e_t = torch.tensor(np.asarray(expect, np.uint32).view(np.int32), device="cuda")
+    dsz, st, crc = batch.decompress(src, out, crc_state=s_t, crc_expect=e_t, max_dsize=16384)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    crc = crc.cpu().numpy().view(np.uint32)
+    for i in range(n):
+        want = O.crc32_write(states[i], comps[i]) ^ 0xFFFFFFFF
+        assert int(crc[i]) == want, i
+        assert st[i] == (_lib.E_CRC if i in bad else _lib.OK), (i, st[i])
+    got = out.to_bytes(dsz.cpu().numpy())
+    for i in range(n):
+        if i not in bad:
+            assert got[i] == plains[i], i

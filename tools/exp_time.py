@@ -24,7 +24,10 @@ idx = torch.from_numpy(np.arange(n) % uniq).to(dev)
 src = batch.BlockBatch(comp.data, comp.off[idx], cs[idx])
 out = batch.BlockBatch.empty_for([bs] * n, device=dev)
 ws = batch.Workspace(dev)
-dsz, st, _ = batch.decompress(src, out, max_dsize=bs, workspace=ws)
+kw = {}
+if os.environ.get("QLZX_CRC"):   # time the fused record-CRC verify (K1) as well
+    kw = dict(crc_state=torch.full((n,), -1, dtype=torch.int32, device=dev), crc_expect=batch.crc32(src))
+dsz, st, _ = batch.decompress(src, out, max_dsize=bs, workspace=ws, **kw)
 torch.cuda.synchronize()
 exp = bool(os.environ.get("QLZX_EXPERIMENT"))
 ok = int((st != 0).sum()) == 0 and torch.equal(out.data[: uniq * bs], plain.data[: uniq * bs])
@@ -34,10 +37,10 @@ ts = []
 for _ in range(reps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    batch.decompress(src, out, max_dsize=bs, workspace=ws)
+    batch.decompress(src, out, max_dsize=bs, workspace=ws, **kw)
     e1.record()
     torch.cuda.synchronize()
     ts.append(e0.elapsed_time(e1))
 ms = float(np.median(ts))
-print(f"{os.path.basename(os.environ.get('QLZX_LIB', 'libqlzx.so'))}: {n} x {bs}: {ms:.3f} ms "
+print(f"{os.path.basename(os.environ.get('QLZX_LIB', 'libqlzx.so'))}{' +crc' if kw else ''}: {n} x {bs}: {ms:.3f} ms "
       f"({n * bs / ms / 1e6 / 1.073741824:.1f} GiB/s out) roundtrip={'ok' if ok else 'BAD'}")

@@ -48,6 +48,64 @@ def k1_groups(c: bytes):
     return recs, n, dsize, hdr
 
 
+def k1_events(c: bytes, gmax=None):
+    """k_dec_parse's event loop (csrc/qlzx_decode_wave.hip), one lane: (recs, nitems, ok)."""
+    hdr = 9 if c[0] & 2 else 3
+    dsize = int.from_bytes(c[5:9], "little") if hdr == 9 else c[2]
+    csize = len(c)
+    if gmax is None:
+        gmax = min(dsize, 65536) // 31 + 2
+    cp = c + bytes(8)
+    ip, g, gcw, mrem, extra, m, ra, rb, klast, needcw = hdr, 0, 0, 0, 0, 0, 0, 0, 31, True
+    recs = []
+    while True:
+        kM = (mrem | 0x80000000) & -(mrem | 0x80000000)
+        kM = kM.bit_length() - 1
+        posM = gcw + 4 + kM + extra
+        cwEnd = needcw and ip + 4 > csize
+        mEnd = (not needcw) and posM >= csize
+        if cwEnd:
+            break
+        rpos = ip if needcw else posM
+        w = int.from_bytes(cp[rpos:rpos + 4], "little")
+        cwEv = needcw
+        mEv = (not needcw) and not mEnd
+        ty = (w & 3) + (1 if (w & 127) == 3 else 0)
+        code = (0x32110 >> (ty * 4)) & 15
+        bad = (cwEv and ((w >> 31) == 0 or g >= gmax)) or (mEv and posM + code + 1 > csize)
+        if bad:
+            return recs, 0, False
+        bit = 1 << kM
+        ngcw = ip if cwEv else gcw
+        nmrem = (w & 0x7fffffff) if cwEv else ((mrem & ~bit) if mEv else mrem)
+        nextra = 0 if cwEv else (extra + code if mEv else extra)
+        nm = 0 if cwEv else (m | bit if mEv else m)
+        na = 0 if cwEv else (ra | bit if mEv and code & 1 else ra)
+        nb = 0 if cwEv else (rb | bit if mEv and code & 2 else rb)
+        ng = g + 1 if cwEv else g
+        gend = ngcw + 35 + nextra
+        close = (cwEv or mEv) and nmrem == 0
+        partial = close and gend > csize
+        if close or mEnd:
+            while len(recs) < ng:
+                recs.append(None)
+            recs[ng - 1] = (ngcw, nm, na, nb)
+        if mEnd:
+            klast = kM - (posM - csize)
+        elif partial:
+            klast = 31 - (gend - csize)
+        g, gcw, mrem, extra, m, ra, rb = ng, ngcw, nmrem, nextra, nm, na, nb
+        if mEnd or partial:
+            break
+        if close:
+            ip, needcw = gend, True
+        else:
+            needcw = False
+    if g == 0:
+        return recs, 0, False
+    return recs, (g - 1) * 31 + klast, True
+
+
 def decode_tok(t):
     ty = (t & 3) + ((t & 127) == 3)
     if ty == 0:
@@ -61,8 +119,15 @@ def decode_tok(t):
     return t >> 15, ((t >> 7) & 255) + 3, 4
 
 
-def model(c: bytes, W=4096, MR=256):
-    recs, nitems, dsize, hdr = k1_groups(c)
+def model(c: bytes, W=4096, MR=256, k1=None):
+    if k1 == "events":
+        hdr = 9 if c[0] & 2 else 3
+        dsize = int.from_bytes(c[5:9], "little") if hdr == 9 else c[2]
+        recs, nitems, ok = k1_events(c)
+        if not ok:
+            return "E_CORRUPT(k1)", None
+    else:
+        recs, nitems, dsize, hdr = k1_groups(c)
     csize = len(c)
     cp = c + bytes(8)
     nb = (nitems + 63) // 64
@@ -174,6 +239,35 @@ def model(c: bytes, W=4096, MR=256):
     return "OK", bytes(out[:dsize])
 
 
+def corrupt_check(n=3000, seed=5):
+    """Event-loop K1 + K2 model status/bytes == oracle on corrupted golden streams."""
+    import json
+    import random
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    man = json.load(open(os.path.join(root, "tests", "golden", "golden.json")))
+    blob = open(os.path.join(root, "tests", "golden", "qlz_vectors.bin"), "rb").read()
+    base = [blob[v["c_out"][0]:v["c_out"][0] + v["c_out"][1]] for v in man["vectors"]
+            if v["cls"] in ("text", "runs", "kat") and v["n"] >= 100]
+    rng = random.Random(seed)
+    mism = 0
+    for t in range(n):
+        c = bytearray(rng.choice(base))
+        if not c[0] & 1:
+            continue
+        hdr = 9 if c[0] & 2 else 3
+        k = rng.randrange(hdr, len(c))
+        c[k] = rng.randrange(256)
+        c = bytes(c)
+        ost, od = O.decompress(c)
+        st, y = model(c, k1="events")
+        ok = (st == "OK") == (ost == O.OK) and (st != "OK" or y == od)
+        if not ok:
+            mism += 1
+            if mism < 5:
+                print("mismatch", t, st, ost)
+    print("corrupt cases checked:", n, "mismatches:", mism)
+
+
 def main():
     W = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     MR = int(sys.argv[2]) if len(sys.argv) > 2 else 256
@@ -184,7 +278,7 @@ def main():
         c = O.compress(x)
         if not c[0] & 1:
             continue
-        st, y = model(c, W, MR)
+        st, y = model(c, W, MR, k1="events")
         ok = st == "OK" and y == x
         bad += not ok
         if not ok:
@@ -194,3 +288,4 @@ def main():
 
 if __name__ == "__main__":
     main()
+    corrupt_check()

@@ -48,17 +48,8 @@ names1 = ["pre-loop", "wait DMA", "CRC", "parse", "issue+end"]
 print("K1 per wave per round (cycles):", {nm: round(p[j] / waves_k1 / rounds) for j, nm in enumerate(names1)})
 print("K1 parse iterations per wave-round: %.1f, active lanes per iteration (lane 0 only sampled): %.2f"
       % (p[5] / waves_k1 / rounds, p[6] / max(p[5], 1)))
-names2 = ["literal stores", "prefetch issue", "decode+scan+checks", "sub-rounds", "wait prefetch", "write-out",
-          "bitmap+owner+masks", "far copies"]
-print("K2 per batch (cycles):", {nm: round(p[8 + j] / batches) for j, nm in enumerate(names2)})
-print("K2 per block total (cycles):", round(p[8:16].sum() / n))
-if True:
-    print("K2 seq per block (cycles):", {nm: round(p[8 + j] / n) for j, nm in enumerate(names2[:5])},
-          "sub-batches/block %.1f, sub-rounds/block %.1f" % (p[15] / n, p[14] / n))
-names3 = ["wait DMA", "item decode", "IP scan+checks+writes", "MP steps", "prefetch issue"]
-print("K2 split per IP batch (cycles):", {nm: round(p[16 + j] / batches) for j, nm in enumerate(names3)})
-print("K2 split per block total (cycles):", round(p[16:21].sum() / n))
-names4 = ["coverage", "readiness", "far", "copy", "spec", "carry"]
-steps = max(p[30], 1)
-print("K2 split MP per step (cycles):", {nm: round(p[24 + j] / steps) for j, nm in enumerate(names4)})
-print("K2 split MP steps per block: %.1f, far-load steps per block: %.1f" % (p[30] / n, p[31] / n))
+# K2 = k_dec_bytes: stamps 0..4 are phases, 5..7 counts (slot 1 = p[8:16])
+names2 = ["item phase", "markers+fill", "pointer jumping", "gather", "store"]
+k2 = p[8:16]
+print("K2 per block (cycles):", {nm: round(k2[j] / n) for j, nm in enumerate(names2)}, "total", round(k2[:5].sum() / n))
+print("K2 per block: batches %.1f, marker passes %.1f, pointer-jumping rounds %.1f" % (k2[5] / n, k2[6] / n, k2[7] / n))
