@@ -422,10 +422,19 @@ int decompress1(const char *source, void *destination, size_t *dsize_out) {
     memcpy(h_data, source, csize);
     HIP_OK(hipMemcpyAsync(d_meta, c.h_buf, 256 + csize, hipMemcpyHostToDevice, c.s));
     Meta *dm = (Meta *)d_meta;
-    qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
-    if (int r = qlzx_decompress_batch(&b, &dm->dst_cap, &dm->out_size, &dm->status, nullptr, nullptr, nullptr,
-                                      (uint32_t)dsize, d_ws, ws_b, c.s))
-        return r;
+    if (dsize <= QLZX_FAST_MAX_DSIZE && csize <= qlzx::kSoloMaxCsize) {
+        // the latency path: one workgroup parses and decodes the block (qlzx_decode_solo.hip)
+        static_assert(qlzx::kSoloGmax * sizeof(qlzx::GroupRec) <= (1u << 20), "solo records");
+        if (int r = qlzx::launch_decode_solo(
+                d_src, (uint32_t)csize, d_dst, (uint32_t)dsize, (uint32_t)dsize, (qlzx::GroupRec *)d_ws, &dm->status,
+                &dm->out_size, c.s))
+            return fail(QLZX_R_HIP, "decode_solo launch", (hipError_t)r);
+    } else {
+        qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
+        if (int r = qlzx_decompress_batch(&b, &dm->dst_cap, &dm->out_size, &dm->status, nullptr, nullptr, nullptr,
+                                          (uint32_t)dsize, d_ws, ws_b, c.s))
+            return r;
+    }
     HIP_OK(hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s));
     if (dsize) HIP_OK(hipMemcpyAsync(h_data, d_dst, dsize, hipMemcpyDeviceToHost, c.s));
     HIP_OK(hipStreamSynchronize(c.s));

@@ -59,20 +59,14 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+// One block by one wave (lane = 0..63): src/csize its stream, dst its output, bi/rb what K1
+// (or the solo parse, qlzx_decode_solo.hip) found; the block's status and size go to
+// *status_i / *dsize_i.  kind is kBlkStored or kBlkCompressed.
 template <uint32_t W, uint32_t MR>
-__global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
-                                                  uint32_t first, uint32_t count, const BlkInfo *info,
-                                                  const GroupRec *recs, uint32_t gmax, const uint32_t *list) {
+__device__ __forceinline__ void dec_bytes_block(K2bLds<W, MR> &L, const uint8_t *src, uint8_t *dst,
+                                                uint32_t csize, const BlkInfo bi, const GroupRec *rb,
+                                                int32_t *status_i, uint32_t *dsize_i, uint32_t lane) {
     static_assert(W >= 2 * MR && MR >= kChunk && (W & (W - 1)) == 0 && (MR & (MR - 1)) == 0, "ring sizes");
-    __shared__ __attribute__((aligned(16))) K2bLds<W, MR> L;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t bx = blockIdx.x;  // workspace slot
-    if (bx >= count) return;
-    const uint32_t i = list ? list[bx] : first + bx;  // block
-    const BlkInfo bi = info[bx];
-    if (bi.kind == kBlkSkip) return;
-    const uint8_t *src = b.src + b.src_off[i];
-    uint8_t *dst = b.dst + b.dst_off[i];
     const uint32_t dsize = bi.dsize;
     if (bi.kind == kBlkStored) {  // quicklz.c:808-811
         const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
@@ -86,14 +80,12 @@ __global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize
             }
         }
         for (uint32_t p = p0 + lane; p < dsize; p += 64) dst[p] = s[p];
-        if (lane == 0) { status[i] = QLZX_OK; if (dsize_out) dsize_out[i] = dsize; }
+        if (lane == 0) { *status_i = QLZX_OK; if (dsize_i) *dsize_i = dsize; }
         return;
     }
     for (uint32_t q = lane * 16; q < MR * 2; q += 1024) *(uint4 *)((uint8_t *)L.mk + q) = make_uint4(0, 0, 0, 0);
 
-    const GroupRec *rb = recs + (size_t)bx * gmax;
     const uint32_t nitems = bi.nitems;
-    const uint32_t csize = b.src_len[i];
     const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
     const uint32_t nb = (nitems + 63) / 64;
     const uint32_t tail_from = dsize > QLZX_TAIL ? dsize - 1 - QLZX_TAIL : 0;  // op >= this: tail (quicklz.c:503)
@@ -262,9 +254,23 @@ __global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize
     vm_sync();
     PROF_FLUSH(1);
     if (lane == 0) {
-        status[i] = err ? QLZX_E_CORRUPT : QLZX_OK;
-        if (dsize_out) dsize_out[i] = err ? 0u : dsize;
+        *status_i = err ? QLZX_E_CORRUPT : QLZX_OK;
+        if (dsize_i) *dsize_i = err ? 0u : dsize;
     }
+}
+
+template <uint32_t W, uint32_t MR>
+__global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
+                                                  uint32_t first, uint32_t count, const BlkInfo *info,
+                                                  const GroupRec *recs, uint32_t gmax, const uint32_t *list) {
+    __shared__ __attribute__((aligned(16))) K2bLds<W, MR> L;
+    const uint32_t bx = blockIdx.x;  // workspace slot
+    if (bx >= count) return;
+    const uint32_t i = list ? list[bx] : first + bx;  // block
+    const BlkInfo bi = info[bx];
+    if (bi.kind == kBlkSkip) return;
+    dec_bytes_block<W, MR>(L, b.src + b.src_off[i], b.dst + b.dst_off[i], b.src_len[i], bi,
+                           recs + (size_t)bx * gmax, status + i, dsize_out ? dsize_out + i : nullptr, threadIdx.x);
 }
 
 }  // namespace qlzx

@@ -167,6 +167,31 @@ __global__ void __launch_bounds__(kOrderWG) k_order_scatter(const uint32_t *src_
 }
 
 // ------------------------------------------------------------------ K1 ----
+// Header checks of one block of `len` bytes (quicklz.c:780-811 and the batch API's bounds):
+// the status, and for QLZX_OK its kind (kBlkStored / kBlkCompressed), sizes and header length.
+__device__ __forceinline__ int classify_block(const uint8_t *src, uint32_t len, uint32_t cap, uint32_t max_dsize,
+                                              uint32_t &kind, uint32_t &csize, uint32_t &dsize, uint32_t &hdr) {
+    kind = kBlkSkip;
+    if (len < 3) return QLZX_E_HEADER;
+    hdr = (src[0] & 2u) ? 9u : 3u;
+    if (len < hdr) return QLZX_E_HEADER;
+    const Header h = parse_header(src);
+    csize = h.csize;
+    dsize = h.dsize;
+    if (h.csize != len) return QLZX_E_SIZE_COMPRESSED;
+    if (h.level != 3) return QLZX_E_LEVEL;
+    if (h.dsize > cap) return QLZX_E_DST_CAP;
+    if (h.dsize > max_dsize) return QLZX_E_MAX_DSIZE;     // the caller's bound is wrong
+    if (h.dsize > QLZX_FAST_MAX_DSIZE) return kPending;  // general path owns it
+    if (!h.compressed) {
+        if (csize < hdr + dsize) return QLZX_E_CORRUPT;
+        kind = kBlkStored;
+    } else {
+        kind = kBlkCompressed;
+    }
+    return QLZX_OK;
+}
+
 // Ring layout per wave: [slot][piece 0..3][lane][16 B]; stream byte p of a lane
 // (q = p + shift, shift = src & 15) lives in round q/64, slot (q/64) % 4,
 // piece (q/16) % 4, byte q % 16 -- i.e. at ((q/16) % 16) * 1 KiB + lane * 16 + q % 16.
@@ -219,25 +244,7 @@ __global__ void __launch_bounds__(kParseWG<CRC>) k_dec_parse(qlzx_blocks b, cons
     const uint8_t *src = b.src + b.src_off[i];
     if (inrange) {
         len = b.src_len[i];
-        if (len < 3) st = QLZX_E_HEADER;
-        else {
-            hdr = (src[0] & 2u) ? 9u : 3u;
-            if (len < hdr) st = QLZX_E_HEADER;
-            else {
-                const Header h = parse_header(src);
-                csize = h.csize;
-                dsize = h.dsize;
-                if (h.csize != len) st = QLZX_E_SIZE_COMPRESSED;
-                else if (h.level != 3) st = QLZX_E_LEVEL;
-                else if (dst_cap && h.dsize > dst_cap[i]) st = QLZX_E_DST_CAP;
-                else if (h.dsize > max_dsize) st = QLZX_E_MAX_DSIZE;     // the caller's bound is wrong
-                else if (h.dsize > QLZX_FAST_MAX_DSIZE) st = kPending;  // general path owns it
-                else if (!h.compressed) {
-                    if (csize >= hdr + dsize) kind = kBlkStored;
-                    else st = QLZX_E_CORRUPT;
-                } else kind = kBlkCompressed;
-            }
-        }
+        st = classify_block(src, len, dst_cap ? dst_cap[i] : 0xffffffffu, max_dsize, kind, csize, dsize, hdr);
     }
     const uintptr_t a = (uintptr_t)src;
     const uint8_t *gbase = (const uint8_t *)(a & ~(uintptr_t)15);
@@ -879,6 +886,10 @@ namespace qlzx {
 #define QLZX_K2B_MR 256
 #endif
 constexpr uint32_t kWinB = QLZX_K2B_WIN, kMarkRing = QLZX_K2B_MR;
+
+}  // namespace qlzx
+#include "qlzx_decode_solo.hip"
+namespace qlzx {
 
 inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uint32_t *dsize,
                               int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,

@@ -268,6 +268,116 @@ def corrupt_check(n=3000, seed=5):
     print("corrupt cases checked:", n, "mismatches:", mism)
 
 
+def solo_parse(c: bytes, gmax=None):
+    """k_dec_solo's parse (csrc/qlzx_decode_solo.hip): unchecked speculative group lengths at
+    every byte up to 128 B before the end, the two-group shortcut j2, the chain walk with K1's
+    byte parse where there is no shortcut -> (recs, nitems, ok) like k1_events."""
+    hdr = 9 if c[0] & 2 else 3
+    dsize = int.from_bytes(c[5:9], "little") if hdr == 9 else c[2]
+    csize = len(c)
+    if gmax is None:
+        gmax = min(dsize, 65536) // 31 + 2
+    code = [((0x32110 >> (4 * ((b & 3) + ((b & 127) == 3)))) & 15) for b in c]
+    delta = [0] * csize
+    for x in range(hdr, csize):
+        if x + 128 <= csize:
+            cw = int.from_bytes(c[x:x + 4], "little")
+            if cw >> 31:
+                mrem, extra = cw & 0x7fffffff, 0
+                while mrem:
+                    k = (mrem & -mrem).bit_length() - 1
+                    extra += code[x + 4 + k + extra]
+                    mrem &= mrem - 1
+                delta[x] = 35 + extra
+    j2 = [0] * csize
+    for x in range(hdr, csize):
+        d1 = delta[x]
+        d2 = delta[x + d1] if d1 and x + d1 < csize else 0
+        j2[x] = d1 + d2 - 69 if d2 else 0
+    x, glist, klast = hdr, [], 31
+    while True:
+        if x + 4 > csize:
+            break
+        if j2[x] and len(glist) + 2 <= gmax:
+            glist += [x, x + delta[x]]
+            x += j2[x] + 69
+            continue
+        if len(glist) >= gmax:
+            return [], 0, False
+        glist.append(x)
+        if delta[x]:
+            x += delta[x]
+            continue
+        cw = int.from_bytes(c[x:x + 4], "little")
+        if not cw >> 31:
+            return [], 0, False
+        p, k = x + 4, 0
+        while k < 31 and p < csize:
+            cc = code[p] if (cw >> k) & 1 else 0
+            if p + cc + 1 > csize:
+                return [], 0, False
+            p += cc + 1
+            k += 1
+        if k < 31:
+            klast = k
+            break
+        x = p
+    if not glist:
+        return [], 0, False
+    recs = []
+    for g, x in enumerate(glist):
+        cw = int.from_bytes(c[x:x + 4], "little")
+        nk = klast if g + 1 == len(glist) else 31
+        m = cw & ((1 << nk) - 1)
+        mrem, extra, a, b = m, 0, 0, 0
+        while mrem:
+            k = (mrem & -mrem).bit_length() - 1
+            pos = x + 4 + k + extra
+            a |= (code[pos] & 1) << k
+            b |= ((code[pos] >> 1) & 1) << k
+            extra += code[pos]
+            mrem &= mrem - 1
+        recs.append((x, m, a, b))
+    return recs, (len(glist) - 1) * 31 + klast, True
+
+
+def solo_check(n=3000, seed=7):
+    """solo_parse == k1_events (records, item count, status) on valid and corrupted streams."""
+    import json
+    import random
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    man = json.load(open(os.path.join(root, "tests", "golden", "golden.json")))
+    blob = open(os.path.join(root, "tests", "golden", "qlz_vectors.bin"), "rb").read()
+    base = [blob[v["c_out"][0]:v["c_out"][0] + v["c_out"][1]] for v in man["vectors"]
+            if v["cls"] in ("text", "runs", "kat") and v["n"] >= 20]
+    base = [b for b in base if b[0] & 1]
+    rng = random.Random(seed)
+    mism = 0
+    for t in range(n + len(base)):
+        c = bytearray(base[t] if t < len(base) else rng.choice(base))
+        if t >= len(base):
+            for _ in range(rng.choice((1, 1, 2, 3))):
+                hdr = 9 if c[0] & 2 else 3
+                k = rng.randrange(hdr, len(c))
+                c[k] = rng.randrange(256)
+            if rng.random() < 0.2:   # truncated (csize field rewritten to match)
+                cut = rng.randrange((9 if c[0] & 2 else 3) + 1, len(c) + 1)
+                c = c[:cut]
+                if c[0] & 2:
+                    c[1:5] = len(c).to_bytes(4, "little")
+                else:
+                    c[1] = len(c)
+        c = bytes(c)
+        r1, n1, ok1 = k1_events(c)
+        r2, n2, ok2 = solo_parse(c)
+        same = ok1 == ok2 and (not ok1 or (n1 == n2 and r1[:len(r2)] == r2 and len(r1) == len(r2)))
+        if not same:
+            mism += 1
+            if mism < 5:
+                print("solo mismatch", t, ok1, ok2, n1, n2, len(r1), len(r2))
+    print("solo parse cases checked:", n + len(base), "mismatches:", mism)
+
+
 def main():
     W = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     MR = int(sys.argv[2]) if len(sys.argv) > 2 else 256
@@ -287,5 +397,8 @@ def main():
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["solo"]:
+        solo_check()
+        sys.exit(0)
     main()
     corrupt_check()
