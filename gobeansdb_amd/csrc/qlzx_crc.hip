@@ -145,6 +145,77 @@ __device__ uint32_t wave_crc(const uint32_t *lds, const uint8_t *p, uint64_t len
     return __shfl(c, 0, 64);
 }
 
+// ---- wave_crc_b16: wave_crc with the byte table replicated per LDS bank ----
+// Same layout, initial-state fold and lane-combine tree as wave_crc, but each lane runs its 64-B
+// piece through ONE byte table (c = T[(c ^ b) & 0xff] ^ c >> 8) held 16 times over, lane l
+// reading copy l % 16: entry e of copy q sits at dword 16 e + q, i.e. bank q + 16 (e & 1) of the
+// 32 a half-wave uses, so only lanes l and l + 16 can collide (one extra cycle half the time).
+// slice8's eight tables serve random indices at about four conflicts per half-wave: the lookups,
+// not the data, bound it (1 lookup per byte either way).  LDS: the replicated table, then the
+// g_crc_mul tables (kCrcB16LdsWords).
+constexpr uint32_t kCrcB16LdsWords = 16 * 256 + kMulTabs * 1024;
+
+__device__ __forceinline__ void load_crc_b16_lds(uint32_t *lds) {
+    for (uint32_t i = threadIdx.x; i < 16 * 256; i += blockDim.x) lds[i] = g_crc_table[i >> 4];
+    for (uint32_t i = threadIdx.x; i < kMulTabs * 1024; i += blockDim.x) lds[16 * 256 + i] = g_crc_mul[i];
+}
+
+__device__ uint32_t wave_crc_b16(const uint32_t *lds, const uint8_t *p, uint64_t len, uint32_t init, uint32_t lane) {
+    const uint32_t *t16 = lds + (lane & 15), *mul = lds + 16 * 256;
+    if (len < 4) {
+        uint32_t c = init;
+        for (uint32_t b = 0; b < len; b++) c = t16[((c ^ p[b]) & 0xffu) << 4] ^ (c >> 8);
+        return c;
+    }
+    const uint32_t m = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t *w32 = (const uint32_t *)(p - m);
+    const uint64_t nst = (len + kStripe - 1) / kStripe;
+    const uint32_t pad = (uint32_t)(nst * kStripe - len);
+    const uint32_t sh = (m - pad) & 3u;
+    const int64_t lastdw = (int64_t)((len + m - 1) >> 2);
+    const uint64_t ini = (uint64_t)init << (8 * m);
+    const uint32_t keep0 = 0xffffffffu << (8 * m);
+    uint32_t c = 0;
+    for (uint64_t t = 0; t < nst; t++) {
+        const int64_t a = (int64_t)(t * kStripe + kPiece * lane) - (int64_t)pad + m;
+        c = crc_mul_tab(mul + 6 * 1024, c);
+        if (a + (int64_t)kPiece <= (int64_t)m) continue;
+        const int64_t d0 = (a - (int64_t)sh) >> 2;
+        uint32_t w[17];
+        if (d0 >= 2 && d0 + 16 <= lastdw) {
+            const uint4 *q4 = (const uint4 *)(w32 + d0);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint4 v = q4[k];
+                w[4 * k] = v.x, w[4 * k + 1] = v.y, w[4 * k + 2] = v.z, w[4 * k + 3] = v.w;
+            }
+            w[16] = sh ? w32[d0 + 16] : 0u;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 17; k++) {
+                const int64_t i = d0 + k;
+                uint32_t v = (i >= 0 && i <= lastdw) ? w32[i] : 0u;
+                if (i == 0) v = (v & keep0) ^ (uint32_t)ini;
+                if (i == 1) v ^= (uint32_t)(ini >> 32);
+                w[k] = v;
+            }
+        }
+        if (sh) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) w[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            c ^= w[k];
+#pragma unroll
+            for (int b = 0; b < 4; b++) c = t16[(c & 0xffu) << 4] ^ (c >> 8);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) c = crc_mul_tab(mul + k * 1024, c) ^ __shfl_xor(c, 1 << k, 64);
+    return __shfl(c, 0, 64);
+}
+
 __global__ void __launch_bounds__(256) k_crc32(const uint8_t *src, const uint64_t *off,
                                                const uint32_t *len, uint32_t n,
                                                const uint32_t *init, uint32_t final_xor,

@@ -2,9 +2,10 @@
 // (one CHUNK) at a time, 4 bytes per lane, each byte gathered from the position it copies.
 //
 // K1 (k_dec_parse, qlzx_decode_wave.hip) still walks the serial control-word chain and emits
-// one GroupRec per control word.  This kernel replaces the item-per-lane K2 (k_dec_blocks),
-// whose cost was the per-item 16-B masked copies and their readiness sub-rounds (≈580
-// instructions per 64 items).  Here the work per output byte is a gather:
+// one GroupRec per control word.  This kernel replaced the item-per-lane K2 of rounds 1-2
+// (k_dec_blocks, removed in round 3), whose cost was the per-item 16-B masked copies and their
+// readiness sub-rounds (≈580 instructions per 64 items).  Here the work per output
+// byte is a gather:
 //
 //   ITEM PHASE (64 items per batch, one per lane; quicklz.c:513-671 restated item-parallel):
 //     token position from the GroupRec (ip + 4 + k + popc(a & low(k)) + 2 popc(b & low(k))),
