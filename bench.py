@@ -82,7 +82,7 @@ def parse():
                    help="skip the \"crc\" leg (the c2 shard again with the fused CRC verify)")
     p.add_argument("--traffic-json", default=None,
                    help="PMC HBM bytes per block (tools/traffic.py output); default: the committed "
-                        "profiles/r02b_c2_traffic.json for the c2 workload")
+                        "profiles/r03_c2_traffic.json for the c2 workload")
     return p.parse_args()
 
 
@@ -256,11 +256,15 @@ def main():
     achieved = (csum + dsum) / (kern_ms * 1e-3) / 1e9
     traffic = None
     if args.traffic_json is None and args.mode == "decompress" and kind == "text" and bs == 16384 and not args.crc:
-        args.traffic_json = os.path.join(ROOT, "profiles", "r02b_c2_traffic.json")
+        args.traffic_json = os.path.join(ROOT, "profiles", "r03_c2_traffic.json")
+    traffic_src = None
     if args.traffic_json and os.path.exists(args.traffic_json):
-        # PMC-measured HBM bytes per block (tools/traffic.py) x blocks per launch
+        # PMC-measured HBM bytes per block (tools/traffic.py) x blocks per launch: a committed
+        # measurement of this workload (FETCH_SIZE x 2 + WRITE_SIZE passes), not a counter of this run
         tj = json.load(open(args.traffic_json))
         traffic = round(tj["hbm_bytes_per_block"] * n)
+        traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: {tj['hbm_bytes_per_block']:.0f} B/block "
+                       f"(PMC, committed) x {n} blocks")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N = 1 only
@@ -290,7 +294,7 @@ def main():
                        "fused_crc": bool(args.crc), "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel_ms": round(kern_ms, 4),
+                         "traffic_source": traffic_src, "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_launch": csum + dsum},
             "cpu_baseline": cpu,
         }
@@ -467,9 +471,12 @@ def bench_compress(args, rank, world, dev, kind, emit: bool = True):
     value = tot["in_bytes"] * args.steps / wall / 2**30
     achieved = (n * bs + csum) / (kern_ms * 1e-3) / 1e9
     traffic = None
-    tj = args.traffic_json or os.path.join(ROOT, "profiles", "r02b_c3_traffic.json")
+    traffic_src = None
+    tj = args.traffic_json or os.path.join(ROOT, "profiles", "r03_c3_traffic.json")
     if os.path.exists(tj) and kind == "image" and bs == 65536:
-        traffic = round(json.load(open(tj))["hbm_bytes_per_block"] * n)
+        tpb = json.load(open(tj))["hbm_bytes_per_block"]
+        traffic = round(tpb * n)
+        traffic_src = f"{os.path.relpath(tj, ROOT)}: {tpb:.0f} B/block (PMC, committed) x {n} blocks"
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N = 1 only
         ns = min(256, n)
@@ -492,7 +499,8 @@ def bench_compress(args, rank, world, dev, kind, emit: bool = True):
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": n * bs + csum},
+                         "traffic_source": traffic_src, "kernel_ms": round(kern_ms, 4),
+                         "algorithmic_bytes_per_launch": n * bs + csum},
             "cpu_baseline": cpu,
         }
         if emit:
