@@ -362,6 +362,10 @@ thread_local Ctx t_ctx;
 
 thread_local int t_last_status = QLZX_OK;
 
+#ifndef QLZX_SOLO_ENC_CAP
+#define QLZX_SOLO_ENC_CAP 65536u
+#endif
+
 // One block through the batch encoder.  Returns a qlzx_return code (runtime failure) and sets
 // *csize (0 with t_last_status != OK when the kernel rejects the block).
 int compress1(const void *source, char *destination, size_t size, uint32_t flags, size_t *csize) {
@@ -369,8 +373,11 @@ int compress1(const void *source, char *destination, size_t size, uint32_t flags
     Ctx &c = t_ctx;
     if (int r = c.init()) return r;
     const bool l1 = (flags & QLZX_F_LEVEL1) != 0;
+    // a lone block gets the widest encoder workgroup whatever its size (max_len only picks the
+    // kernel: a 4 KiB block on the 64-thread k_encode_wg<4096> is one wave walking every phase)
+    const uint32_t max_len = size <= QLZX_SOLO_ENC_CAP ? QLZX_SOLO_ENC_CAP : (uint32_t)size;
     const size_t src_b = align_up(size, 256), dst_b = align_up(size + 400, 256);
-    const size_t ws_b = l1 ? qlzx_go_l1_workspace_size(1) : qlzx_compress_workspace_size(1, (uint32_t)size);
+    const size_t ws_b = l1 ? qlzx_go_l1_workspace_size(1) : qlzx_compress_workspace_size(1, max_len);
     // pinned: [meta | src staging, reused for the result]
     if (int r = c.reserve(256 + src_b + dst_b + ws_b, 256 + std::max(src_b, dst_b))) return r;
     uint8_t *d_meta = c.d_buf, *d_src = d_meta + 256, *d_dst = d_src + src_b, *d_ws = d_dst + dst_b;
@@ -384,8 +391,8 @@ int compress1(const void *source, char *destination, size_t size, uint32_t flags
     Meta *dm = (Meta *)d_meta;
     qlzx_blocks b{d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, 1};
     if (int r = l1 ? qlzx_go_l1_compress_batch(&b, &dm->out_size, &dm->status, d_ws, ws_b, c.s)
-                   : qlzx_compress_batch(&b, &dm->out_size, &dm->status, nullptr, nullptr, (uint32_t)size, flags,
-                                         d_ws, ws_b, c.s))
+                   : qlzx_compress_batch(&b, &dm->out_size, &dm->status, nullptr, nullptr, max_len, flags, d_ws,
+                                         ws_b, c.s))
         return r;
     // one D2H of descriptor + the largest possible result, then the only synchronisation
     HIP_OK(hipMemcpyAsync(c.h_buf, d_meta, sizeof(Meta), hipMemcpyDeviceToHost, c.s));
