@@ -127,3 +127,32 @@ def test_wg_encoder_round_trip_on_device(cuda):
     for i in (0, 1, 2, 3, 1000, 2047):
         assert h[i] == O.compress(O.gen_image(77, i, bs))
 
+
+
+def _copy_block(rng, n, frac):
+    """Random bytes with one earlier stretch of frac * n bytes repeated once: few repeated
+    3-grams (so the prefix-first pass is tried) but long matches, so the first bail-out test
+    past 3/4 of the input may pass and the block takes the full pass after all."""
+    a = bytearray(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    k = int(n * frac)
+    a[k:2 * k] = a[:k]
+    return bytes(a)
+
+
+@pytest.mark.parametrize("n", [16384, 40000, 65536])
+def test_wg_encoder_prefix_first_pass(cuda, n):
+    """The prefix-first pass (phase 4 of k_encode_wg): poorly compressible blocks parse only the
+    positions below 3/4 of the input + 1 KiB first and are stored if the first bail-out test
+    fails there (quicklz.c:216-219); otherwise the whole block is encoded.  Noise fractions
+    around the bail-out boundary and the repeat-count threshold, and blocks whose first test
+    passes (long copies) or that never bail, all against the oracle."""
+    rng = np.random.default_rng(n + 5)
+    blocks = []
+    for frac in (0.2, 0.3, 0.35, 0.38, 0.4, 0.42, 0.44, 0.46, 0.5, 0.6):
+        for seed in range(3):
+            blocks.append(_noisy(rng, O.gen_text(40 + seed, int(frac * 1000), n), frac))
+    for frac in (0.1, 0.14, 0.17, 0.2, 0.25):
+        blocks.append(_copy_block(rng, n, frac))
+    outs = _check(blocks, max_len=65536)
+    kinds = [o[0] & 1 for o in outs]  # header bit 0: compressed
+    assert 0 < sum(kinds) < len(kinds), kinds  # both stored and compressed outcomes are covered
