@@ -247,7 +247,7 @@ def main():
                    "ms_per_step": round(wall_c * 1e3 / args.steps, 4),
                    "vs_value": round((tot["out_bytes"] * args.steps / wall_c) / (tot["out_bytes"] * args.steps / wall), 4),
                    "what": "the c2 shard decoded with the record CRC32 of every block computed in the same "
-                           "call (k_dec_crc beside the decode) and verified against crc_expect before its "
+                           "call (fused into the decode kernel K2) and verified against crc_expect before its "
                            "decode (read path of store/datafile.go:161-168)"}
         del cst, cexp
 

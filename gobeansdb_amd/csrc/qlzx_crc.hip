@@ -145,26 +145,23 @@ __device__ uint32_t wave_crc(const uint32_t *lds, const uint8_t *p, uint64_t len
     return __shfl(c, 0, 64);
 }
 
-// ---- wave_crc_b16: wave_crc with the byte table replicated per LDS bank ----
+// ---- wave_crc_rep: wave_crc with the byte table replicated across LDS banks ----
 // Same layout, initial-state fold and lane-combine tree as wave_crc, but each lane runs its 64-B
-// piece through ONE byte table (c = T[(c ^ b) & 0xff] ^ c >> 8) held 16 times over, lane l
-// reading copy l % 16: entry e of copy q sits at dword 16 e + q, i.e. bank q + 16 (e & 1) of the
-// 32 a half-wave uses, so only lanes l and l + 16 can collide (one extra cycle half the time).
-// slice8's eight tables serve random indices at about four conflicts per half-wave: the lookups,
-// not the data, bound it (1 lookup per byte either way).  LDS: the replicated table, then the
-// g_crc_mul tables (kCrcB16LdsWords).
-constexpr uint32_t kCrcB16LdsWords = 16 * 256 + kMulTabs * 1024;
-
-__device__ __forceinline__ void load_crc_b16_lds(uint32_t *lds) {
-    for (uint32_t i = threadIdx.x; i < 16 * 256; i += blockDim.x) lds[i] = g_crc_table[i >> 4];
-    for (uint32_t i = threadIdx.x; i < kMulTabs * 1024; i += blockDim.x) lds[16 * 256 + i] = g_crc_mul[i];
-}
-
-__device__ uint32_t wave_crc_b16(const uint32_t *lds, const uint8_t *p, uint64_t len, uint32_t init, uint32_t lane) {
-    const uint32_t *t16 = lds + (lane & 15), *mul = lds + 16 * 256;
+// piece through ONE byte table (c = T[(c ^ b) & 0xff] ^ c >> 8) held R times over, lane l reading
+// copy l % R: entry e of copy q sits at dword R e + q.  R = 4 (inside K2, in its 4 KiB window):
+// bank q + 4 (e & 7) of the 32 a half-wave uses, eight lanes per copy over eight banks (R = 16
+// would leave only lanes l and l + 16 to collide but needs 16 KiB).  slice8's eight tables serve
+// random indices at about four conflicts per half-wave: the lookups, not the data, bound it (one
+// lookup per byte either way).  mul = the g_crc_mul tables (LDS or global).  The two 32-B halves
+// of a piece run as two independent chains (the lookups are a dependent-latency chain), joined
+// through g_crc_mul32 (global).
+template <uint32_t R>
+__device__ uint32_t wave_crc_rep(const uint32_t *tab, const uint32_t *mul, const uint8_t *p, uint64_t len,
+                                 uint32_t init, uint32_t lane) {
+    const uint32_t *tr = tab + (lane & (R - 1));
     if (len < 4) {
         uint32_t c = init;
-        for (uint32_t b = 0; b < len; b++) c = t16[((c ^ p[b]) & 0xffu) << 4] ^ (c >> 8);
+        for (uint32_t b = 0; b < len; b++) c = tr[((c ^ p[b]) & 0xffu) * R] ^ (c >> 8);
         return c;
     }
     const uint32_t m = (uint32_t)((uintptr_t)p & 3u);
@@ -204,12 +201,18 @@ __device__ uint32_t wave_crc_b16(const uint32_t *lds, const uint8_t *p, uint64_t
 #pragma unroll
             for (int k = 0; k < 16; k++) w[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
         }
+        uint32_t d = 0;
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
+        for (int k = 0; k < 8; k++) {
             c ^= w[k];
+            d ^= w[k + 8];
 #pragma unroll
-            for (int b = 0; b < 4; b++) c = t16[(c & 0xffu) << 4] ^ (c >> 8);
+            for (int b = 0; b < 4; b++) {
+                c = tr[(c & 0xffu) * R] ^ (c >> 8);
+                d = tr[(d & 0xffu) * R] ^ (d >> 8);
+            }
         }
+        c = crc_mul_tab(g_crc_mul32, c) ^ d;
     }
 #pragma unroll
     for (int k = 0; k < 6; k++) c = crc_mul_tab(mul + k * 1024, c) ^ __shfl_xor(c, 1 << k, 64);

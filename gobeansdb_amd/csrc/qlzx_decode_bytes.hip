@@ -260,14 +260,40 @@ __device__ __forceinline__ void dec_bytes_block(K2bLds<W, MR> &L, const uint8_t 
     }
 }
 
-template <uint32_t W, uint32_t MR>
+// CRC: the record CRC (store/datafile.go:161-168) is verified first, over all src_len bytes from
+// crc_state (or ~0), with the byte table four times over in the window (wave_crc_rep<4>) and the
+// g_crc_mul tables read from global memory; a mismatch sets QLZX_E_CRC and nothing is decoded.
+template <uint32_t W, uint32_t MR, bool CRC>
 __global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                                                   uint32_t first, uint32_t count, const BlkInfo *info,
-                                                  const GroupRec *recs, uint32_t gmax, const uint32_t *list) {
+                                                  const GroupRec *recs, uint32_t gmax, const uint32_t *list,
+                                                  const uint32_t *crc_state, const uint32_t *crc_expect,
+                                                  uint32_t *crc_out) {
     __shared__ __attribute__((aligned(16))) K2bLds<W, MR> L;
     const uint32_t bx = blockIdx.x;  // workspace slot
     if (bx >= count) return;
     const uint32_t i = list ? list[bx] : first + bx;  // block
+    if constexpr (CRC) {
+        static_assert(W >= 4096, "the 4-fold CRC table fills 4 KiB of the window");
+        const uint32_t lane = threadIdx.x;
+        uint32_t *tab = (uint32_t *)L.win;
+        for (uint32_t e = lane; e < 256; e += 64) {
+            const uint32_t v = g_crc_table[e];
+            *(uint4 *)(tab + 4 * e) = make_uint4(v, v, v, v);
+        }
+        __syncthreads();
+        const uint32_t c = ~wave_crc_rep<4>(tab, g_crc_mul, b.src + b.src_off[i], b.src_len[i],
+                                            crc_state ? crc_state[i] : 0xffffffffu, lane);
+        __syncthreads();  // the window is the decode's again
+        if (lane == 0 && crc_out) crc_out[i] = c;
+        if (crc_expect && c != crc_expect[i]) {
+            if (lane == 0) {
+                status[i] = QLZX_E_CRC;
+                if (dsize_out) dsize_out[i] = 0;
+            }
+            return;
+        }
+    }
     const BlkInfo bi = info[bx];
     if (bi.kind == kBlkSkip) return;
     dec_bytes_block<W, MR>(L, b.src + b.src_off[i], b.dst + b.dst_off[i], b.src_len[i], bi,

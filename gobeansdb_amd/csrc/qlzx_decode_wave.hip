@@ -15,15 +15,14 @@
 //     base is wave-uniform and no register waits on in-flight loads.  A lane
 //     parses until it runs out of landed bytes, so rounds self-align by bytes.
 //
-// k_dec_crc (only when a record CRC is asked for) one WAVE per block, the
-//     record CRC of store/datafile.go:66-76 over the stored bytes; a mismatch
-//     marks the block QLZX_E_CRC before K2 runs (the read path verifies first).
+// K2 k_dec_bytes (qlzx_decode_bytes.hip) one WAVE per block: when a record CRC
+//     is asked for it is verified first (store/datafile.go:161-168, the CRC of
+//     store/datafile.go:66-76 over the stored bytes; a mismatch is QLZX_E_CRC
+//     and nothing is written); then items are decoded 64 at a time, leaving one
+//     marker per item, and output is produced 256 bytes at a time, every byte
+//     gathered from the position it copies.
 //
-// K2 k_dec_bytes (qlzx_decode_bytes.hip) one WAVE per block: items decoded 64
-//     at a time leave one marker per item; output is then produced 256 bytes at
-//     a time, every byte gathered from the position it copies.
-//
-// K1 of chunk c+1 (and its CRC) run on a side stream beside K2 of chunk c.
+// K1 of chunk c+1 runs on a side stream beside K2 of chunk c.
 #include "qlzx_device.h"
 
 #ifndef QLZX_FAST_MAX_DSIZE
@@ -320,39 +319,6 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
     info[lin] = bi;
 }
 
-// ----------------------------------------------------------- record CRC ----
-// Record CRC of every block of a chunk (the read path verifies it before decoding,
-// store/datafile.go:161-168): one wave per block, wave_crc_b16 (qlzx_crc.hip) over all src_len
-// bytes from crc_state (or ~0), persistent waves over the chunk's list so each 512-thread workgroup
-// loads its 44 KiB of tables once.  It runs after K1 of the chunk and before K2, on K1's side
-// stream (so beside K2 of the previous chunk): a mismatch sets QLZX_E_CRC (over any status K1
-// left, as before the decode) and marks the block skipped for K2.  Round 3 measured (c2 + CRC,
-// one box): the CRC inside K1 (per-lane slicing-by-8) 36.2-36.6 ms, this kernel with
-// slicing-by-8 34.2, with the bank-replicated byte table 33.6-34.0, against 30.2 without a CRC.
-constexpr uint32_t kCrcWG = 512, kCrcGridMax = 1024;
-__global__ void __launch_bounds__(kCrcWG) k_dec_crc(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
-                                                    const uint32_t *crc_state, const uint32_t *crc_expect,
-                                                    uint32_t *crc_out, uint32_t first, uint32_t count, BlkInfo *info,
-                                                    const uint32_t *order) {
-    __shared__ uint32_t tab[kCrcB16LdsWords];
-    load_crc_b16_lds(tab);
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t nwaves = gridDim.x * (kCrcWG / 64);
-    for (uint32_t lin = blockIdx.x * (kCrcWG / 64) + threadIdx.x / 64; lin < count; lin += nwaves) {
-        const uint32_t i = order ? order[lin] : first + lin;
-        const uint32_t c = ~wave_crc_b16(tab, b.src + b.src_off[i], b.src_len[i],
-                                         crc_state ? crc_state[i] : 0xffffffffu, lane);
-        if (lane == 0) {
-            if (crc_out) crc_out[i] = c;
-            if (crc_expect && c != crc_expect[i]) {
-                status[i] = QLZX_E_CRC;
-                if (dsize_out) dsize_out[i] = 0;
-                info[lin].kind = kBlkSkip;
-            }
-        }
-    }
-}
 
 // --------------------------------------------- K2 helpers (qlzx_decode_bytes.hip) ----
 // Per-lane coordinates of item I = 64 bt + lane: group g = I / 31, index k = I % 31.
@@ -488,15 +454,14 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
         hipLaunchKernelGGL(k_dec_parse, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b, dst_cap,
                            dsize, status, first, cnt, info, recs, gmax, order, max_dsize);
-        if (crc) {  // record CRC, verified before K2 decodes (after K1: it overrides K1's statuses)
-            const uint32_t gc = std::min<uint32_t>((cnt + kCrcWG / 64 - 1) / (kCrcWG / 64), kCrcGridMax);
-            hipLaunchKernelGGL(k_dec_crc, dim3(gc), dim3(kCrcWG), 0, s1, b, dsize, status, crc_state, crc_expect,
-                               crc_out, first, cnt, info, order);
-        }
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
         // one kernel for every block size: the LDS window slides over longer blocks
-        hipLaunchKernelGGL((k_dec_bytes<kWinB, kMarkRing>), dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt,
-                           info, recs, gmax, (const uint32_t *)order);
+        if (crc)
+            hipLaunchKernelGGL((k_dec_bytes<kWinB, kMarkRing, true>), dim3(cnt), dim3(64), 0, s, b, dsize, status,
+                               first, cnt, info, recs, gmax, (const uint32_t *)order, crc_state, crc_expect, crc_out);
+        else
+            hipLaunchKernelGGL((k_dec_bytes<kWinB, kMarkRing, false>), dim3(cnt), dim3(64), 0, s, b, dsize, status,
+                               first, cnt, info, recs, gmax, (const uint32_t *)order, nullptr, nullptr, nullptr);
         if (overlap) (void)hipEventRecord(ev_k2[c & 1], s);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;

@@ -139,6 +139,28 @@ static_assert(kMul.t[0] == 0 && kMul.t[6 * 1024 + 256 + 1] == mulmod_c(kTables.p
     M64(i + 896), M64(i + 960)
 __device__ uint32_t g_crc_mul[kMulTabs * 1024] = {M1K(0), M1K(1024), M1K(2048), M1K(3072), M1K(4096),
                                                   M1K(5120), M1K(6144)};
+
+// The same for x^(8 * 32): wave_crc_rep's two half-piece chains meet through it.
+__host__ __device__ constexpr CrcMul make_mul32() {
+    CrcMul m{};
+    const uint32_t k = kTables.byte[32];
+    for (int j = 0; j < 4; j++) {
+        uint32_t bit[8] = {};
+        for (int q = 0; q < 8; q++) bit[q] = mulmod_c(k, 1u << (8 * j + q));
+        for (uint32_t b = 0; b < 256; b++) {
+            uint32_t v = 0;
+            for (int q = 0; q < 8; q++)
+                if (b & (1u << q)) v ^= bit[q];
+            m.t[j * 256 + b] = v;
+        }
+    }
+    return m;
+}
+constexpr CrcMul kMul32 = make_mul32();
+#undef M8
+#define M8(i) kMul32.t[i], kMul32.t[i + 1], kMul32.t[i + 2], kMul32.t[i + 3], kMul32.t[i + 4], kMul32.t[i + 5], \
+    kMul32.t[i + 6], kMul32.t[i + 7]
+__device__ uint32_t g_crc_mul32[1024] = {M1K(0)};
 #undef M1K
 #undef M64
 #undef M8

@@ -1,10 +1,10 @@
 #!/bin/bash
 # Round 3 checkpoint: full GPU suite, the driver's default bench line, rocprof kernel traces of c2
-# decode with and without the record CRC (k_dec_crc), K1/K2 phase stamps (profile build).
+# decode with and without the record CRC (fused into K2), K1/K2 phase stamps (profile build).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r03m; mkdir -p $O
+O=gpurun_out/${OUT:-r03m}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
