@@ -41,6 +41,23 @@
 
 namespace qlzx {
 
+// The thread index behind an opaque move.  Read afresh in every phase, so the compiler cannot hoist
+// tid-derived addresses and lane masks out of the persistent block loop and keep them live (the
+// 64 KiB kernel sits at the 128-VGPR cap of a 1024-thread workgroup: they were what it spilled).
+__device__ __forceinline__ uint32_t tid_here() {
+    uint32_t t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((uint32_t)threadIdx.x));
+    return t;
+}
+
+// An opaque zero: a constant zero register pair or quad is otherwise hoisted out of the block
+// loop and spilled rather than rematerialised.
+__device__ __forceinline__ uint32_t zero_here() {
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+
 __device__ __forceinline__ uint32_t ld32u(const uint8_t *lds, uint32_t a) {
     const uint32_t *w = (const uint32_t *)(lds + (a & ~3u));
     return __builtin_amdgcn_alignbyte(w[1], w[0], a & 3u);
@@ -69,7 +86,7 @@ __device__ __forceinline__ uint64_t shfl_up64(uint64_t x, uint32_t d) {
 // Exclusive block-wide scan of one u64 per thread (W waves); `total` = sum.
 template <uint32_t W>
 __device__ uint64_t block_scan_excl(uint64_t v, uint64_t *wsum, uint64_t &total) {
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t tid0 = tid_here(), lane = tid0 & 63, wave = tid0 >> 6;
     uint64_t x = v;
 #pragma unroll
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -163,7 +180,7 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
     constexpr uint32_t T = 64 * W, NB = 1u << NB_LOG2, NC = NB * W;
     constexpr uint32_t CPT = NC >= T ? NC / T : 1;  // counters per scanning thread
     static_assert(NC % CPT == 0 && NC / CPT <= T, "counter layout");
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tid = tid_here(), lane = tid & 63, wave = tid >> 6;
     const uint64_t ltm = (1ull << lane) - 1ull;
     const uint32_t per = (P + 64 * W - 1) / (64 * W) * 64;
     const uint32_t r0 = min(P, wave * per), r1 = min(P, r0 + per);
@@ -254,7 +271,7 @@ __device__ void bucket_sort(const uint8_t *s_in, uint32_t P, uint16_t *tmp, uint
                             uint32_t *s_cnt, uint32_t *s_hist, uint64_t *wsum, unsigned long long *subA,
                             unsigned long long *subB) {
     constexpr uint32_t T = 64 * W;
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = tid_here();
     uint32_t *cntB = s_cnt, *cntA = s_cnt + cslots(kEncGroups, W);
     for (uint32_t k = tid; k < QLZX_BUCKETS / 2; k += T) s_hist[k] = 0;
     for (uint32_t k = tid; k < cslots(kEncGroups, W); k += T) cntB[k] = 0;
@@ -310,9 +327,9 @@ struct WgCfg {
 // expensive ones spread over the workgroups instead of a static stride.
 __device__ __forceinline__ uint32_t next_block(uint32_t *ticket, uint32_t *s_slot) {
     __syncthreads();  // every thread has read the previous ticket
-    if (threadIdx.x == 0) *s_slot = atomicAdd(ticket, 1u);
+    if (tid_here() == 0) *s_slot = atomicAdd(ticket, 1u);
     __syncthreads();
-    return *s_slot;
+    return __builtin_amdgcn_readfirstlane(*s_slot);  // uniform: the block's pointers and sizes in SGPRs
 }
 
 template <uint32_t CAP>
@@ -327,7 +344,6 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
     __shared__ uint32_t s_misc[24];  // [0] next group, [1] proof count, [4..] CRC stripes
     uint8_t *const s_in = s_u, *const s_l8 = s_u + C::IN_B;
 
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t *gl = (uint32_t *)(ws + (size_t)blockIdx.x * C::SLOT_BYTES);
     uint16_t *goff = (uint16_t *)(gl + CAP);
     uint16_t *bst = goff + CAP;  // sorted-list start of each bucket
@@ -337,6 +353,8 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
     unsigned long long _pacc_sub[16] = {};
 #endif
     for (uint32_t i = next_block(ticket, &s_misc[22]); i < b.n; i = next_block(ticket, &s_misc[22])) {
+        uint32_t tid = tid_here(), lane = tid & 63, wave = tid >> 6;
+#define QLZX_TID_REFRESH() (tid = tid_here(), lane = tid & 63, wave = tid >> 6)
         const uint32_t n = b.src_len[i];  // LDS of the previous block is free (next_block synced)
         if (n > CAP) continue;            // general (lane) path
         if (n == 0) {           // cquicklz.go:36 panics on &src[0]
@@ -351,18 +369,21 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
         const uint8_t *src = b.src + b.src_off[i];
         const uint32_t hdr = n < 216 ? 3u : 9u;  // quicklz.c:708-711
         if (tid == 0) {
-            s_misc[0] = 0;
-            s_misc[1] = 0;
+            const uint32_t z = zero_here();
+            s_misc[0] = z;
+            s_misc[1] = z;
         }
         bool stored = false;
         bool prefix = false;  // try the prefix-only pass first (below, phase 4)
 
         PROF_MARK(0);  // 0: ticket + setup
+        QLZX_TID_REFRESH();
         // ---- S. stored-block proof on incompressible input ----
         if (n >= 256 && (((uintptr_t)src) & 15u) == 0) {
             uint32_t *bm = (uint32_t *)s_u;
             constexpr uint32_t BMW = (1u << C::BM_LOG2) / 32;
-            for (uint32_t k = tid * 4; k < BMW; k += T * 4) *(uint4 *)(bm + k) = make_uint4(0, 0, 0, 0);
+            const uint32_t z0 = zero_here();
+            for (uint32_t k = tid * 4; k < BMW; k += T * 4) *(uint4 *)(bm + k) = make_uint4(z0, z0, z0, z0);
             __syncthreads();
             const uint32_t ny = n - 2;  // positions holding a whole 3-gram
             auto load20 = [&](uint32_t y0, uint32_t w[5]) {
@@ -426,6 +447,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             // at the first control word past 3/4 of the input, so try the prefix alone first
             prefix = !stored && n >= kPrefixMinLen && 100ull * (ny - s_misc[1]) < (uint64_t)kPrefixRepeatPct * ny;
             if (stored) {  // quicklz.c:722-727 from the global copy of the input
+                QLZX_TID_REFRESH();
                 if ((((uintptr_t)dst) & 15u) == 0) {
                     // 16 B per thread per step, four steps' loads in flight before any store
                     // (one dependent load per step made the copy latency-bound: 70 K cycles)
@@ -462,6 +484,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
         uint32_t csz = n + hdr;
         if (!stored) {
             // ---- 0. input -> LDS (zero padded for word over-reads) ----
+            QLZX_TID_REFRESH();
             if ((((uintptr_t)src) & 15u) == 0) {
                 for (uint32_t o = tid * 16; o < n; o += T * 16) {
                     if (o + 16 <= n) *(uint4 *)(s_in + o) = *(const uint4 *)(src + o);
@@ -482,6 +505,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             const uint32_t P = prefix ? min(Pfull, 3u * (n >> 2) + kPrefixMargin) : Pfull;
             if (P) {
                 PROF_MARK(1);  // 1: proof + input load
+                QLZX_TID_REFRESH();
                 // ---- 1. positions sorted by bucket, stable: LSD radix on the low 4 hash
                 //         bits, then on the bucket group (hash >> 4) ----
 #ifdef QLZX_PROFILE
@@ -493,6 +517,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 bucket_sort<W>(s_in, P, goff, gl, bst, s_scr, (uint32_t *)s_l8, s_wsum, subA, subB);
 
                 PROF_MARK(2);  // 2: sort by bucket
+                QLZX_TID_REFRESH();
                 // ---- 2. best match per position, all positions in parallel ----
                 // The candidates of the position at sorted index t are the d most recent
                 // earlier positions of its bucket -- sorted indices t-1 .. t-d -- with
@@ -556,6 +581,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             __syncthreads();
 
             PROF_MARK(3);  // 3: best match per position
+            QLZX_TID_REFRESH();
             // ---- 3. greedy parse (quicklz.c:361-372,449-485): segment walkers + fix-up ----
             const uint32_t nseg = (n + 63) / 64;
             const uint32_t s0 = tid * 64, e0 = min(n, s0 + 64);
@@ -620,7 +646,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     // (runs, repeated stretches), one segment per round.  Such a parse has
                     // few items, so one lane walks it from the start in item steps.
                     uint64_t *sb = (uint64_t *)(s_scr + ((nseg + 1) & ~1u));
-                    for (uint32_t k = tid; k < nseg; k += T) sb[k] = 0;
+                    for (uint32_t k = tid; k < nseg; k += T) sb[k] = zero_here();
                     __syncthreads();
                     if (tid == 0) {
                         for (uint32_t p = 0; p < n;) {
@@ -636,6 +662,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             }
 
             PROF_MARK(4);  // 4: greedy parse
+            QLZX_TID_REFRESH();
             // ---- 4. sizes, bail-out test, emission ----
             uint32_t items = 0, bytes = 0;
             uint32_t szc[4] = {0, 0, 0, 0};  // item sizes - 1, 2 bits per item of the segment (in order)
@@ -708,6 +735,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             }
             bail = __syncthreads_or(bail);
             if (bail) {  // stored block (quicklz.c:722-727)
+                QLZX_TID_REFRESH();
                 if ((((uintptr_t)dst) & 15u) == 0) {  // 16-B stores from the LDS copy of the input
                     const uint32_t tot = n + hdr, a0 = (hdr + 15u) & ~15u, a1 = tot & ~15u;
                     for (uint32_t o = a0 + tid * 16; o < a1; o += T * 16) {
@@ -740,7 +768,11 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                             uint32_t tk;
                             const uint32_t sz = token_of(L, goff[p], tk);
                             atomicOr(&cw[c], 1u << bit);
-                            for (uint32_t k = 0; k < sz; k++) dst[op + k] = (uint8_t)(tk >> (8 * k));
+                            uint8_t *o = dst + op;  // one address, immediate offsets
+                            o[0] = (uint8_t)tk;
+                            if (sz > 1) o[1] = (uint8_t)(tk >> 8);
+                            if (sz > 2) o[2] = (uint8_t)(tk >> 16);
+                            if (sz > 3) o[3] = (uint8_t)(tk >> 24);
                             bb += sz;
                         } else {
                             dst[op] = s_in[p];
@@ -763,11 +795,12 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
         }
 
         PROF_MARK(5);  // 5: sizes/bail/emission (or stored copy)
+        QLZX_TID_REFRESH();
         // ---- 5. fused CRC of the emitted value (store/crc32.go:61-68) ----
         if (crc_state && crc_out) {
             __syncthreads();  // emitted bytes visible to the whole workgroup
             uint32_t *t8 = (uint32_t *)s_l8;
-            load_crc_slice8(t8);
+            for (uint32_t k = tid; k < 8 * 256; k += T) t8[k] = g_crc_slice8[k];
             __syncthreads();
             const uint32_t nst = (csz + 4095) / 4096;
             for (uint32_t st = wave; st < nst; st += W) {
@@ -797,6 +830,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             if (status) status[i] = QLZX_OK;
         }
     }
+#undef QLZX_TID_REFRESH
     PROF_FLUSH(2);
 #ifdef QLZX_PROFILE
     if (g_prof && (threadIdx.x & 63) == 0)
