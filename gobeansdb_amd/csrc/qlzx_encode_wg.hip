@@ -668,24 +668,43 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             uint32_t szc[4] = {0, 0, 0, 0};  // item sizes - 1, 2 bits per item of the segment (in order)
             if (tid < nseg) {
                 items = __popcll(bits);
-                uint32_t j = 0;
-                for (uint64_t t = bits; t;) {  // four items per iteration: their offset loads overlap
+                // Literal items are one byte and leave their 2-bit size code 0, so only the match
+                // items are visited: the segment's positions with a nonzero best length (64 bytes
+                // of s_l8, a nonzero-byte mask per dword), below P, that are items.
+                uint64_t nz = 0;
+                const uint4 *l16 = (const uint4 *)(s_l8 + s0);  // s0 = 64 tid: 16-B aligned
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint4 v = l16[q];
+                    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const uint32_t w = w4[e];
+                        const uint32_t hi = ((((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u) >> 7;
+                        nz |= (uint64_t)((hi * 0x10204080u) >> 28) << (16 * q + 4 * e);  // bit b: byte b != 0
+                    }
+                }
+                const uint32_t keep = P > s0 ? min(64u, P - s0) : 0u;  // positions >= P are never searched
+                nz &= keep >= 64 ? ~0ull : ((1ull << keep) - 1ull);
+                const uint64_t mm = bits & nz;
+                bytes = items - (uint32_t)__popcll(mm);
+                for (uint64_t t = mm; t;) {  // four matches per iteration: their offset loads overlap
                     uint32_t p4[4], L4[4], o4[4];
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
                         p4[u] = t ? s0 + (uint32_t)__builtin_ctzll(t) : 0xFFFFFFFFu;
                         t &= t - 1;
-                        L4[u] = p4[u] < P ? (uint32_t)s_l8[p4[u]] : 0u;
+                        L4[u] = p4[u] != 0xFFFFFFFFu ? (uint32_t)s_l8[p4[u]] : 0u;
                         o4[u] = L4[u] ? (uint32_t)goff[p4[u]] : 0u;
                     }
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
                         if (p4[u] == 0xFFFFFFFFu) break;
                         uint32_t tk;
-                        const uint32_t sz = L4[u] ? token_of(L4[u], o4[u], tk) : 1u;
+                        const uint32_t sz = token_of(L4[u], o4[u], tk);
+                        const uint32_t j = (uint32_t)__popcll(bits & ((1ull << (p4[u] - s0)) - 1ull));  // item rank
                         bytes += sz;
                         szc[j >> 4] |= (sz - 1u) << (2 * (j & 15));
-                        j++;
                     }
                 }
             }
