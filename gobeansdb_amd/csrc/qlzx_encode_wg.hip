@@ -107,6 +107,33 @@ __device__ uint64_t block_scan_excl(uint64_t v, uint64_t *wsum, uint64_t &total)
     return pre + x - v;
 }
 
+// Position (0..63) of the r-th set bit of x (r < popcount(x)), by halving.
+__device__ __forceinline__ uint32_t select64(uint64_t x, uint32_t r) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t w = 32; w >= 1; w >>= 1) {
+        const uint32_t c = (uint32_t)__popcll(x & ((1ull << w) - 1ull));
+        if (r >= c) {
+            r -= c;
+            x >>= w;
+            pos += w;
+        }
+    }
+    return pos;
+}
+
+// Sum of the first r 2-bit fields of the 64-item code array sc[4] (16 fields per word).
+__device__ __forceinline__ uint32_t fields2_prefix(const uint32_t sc[4], uint32_t r) {
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t lim = r > 16 * q ? min(r - 16 * q, 16u) : 0u;  // fields of word q below r
+        const uint32_t w = sc[q] & (lim >= 16 ? 0xFFFFFFFFu : ((1u << (2 * lim)) - 1u));
+        s += (uint32_t)__popc(w & 0x55555555u) + 2u * (uint32_t)__popc(w & 0xAAAAAAAAu);
+    }
+    return s;
+}
+
 // Level-3 match token (quicklz.c:377-406); returns its byte count.
 __device__ __forceinline__ uint32_t token_of(uint32_t ml, uint32_t off, uint32_t &t) {
     if (ml == 3 && off <= 63) { t = off << 2; return 1; }
@@ -476,7 +503,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 } else {
                     for (uint32_t o = tid; o < n; o += T) dst[hdr + o] = src[o];
                 }
-                if (tid == 0) write_header(dst, hdr, false, n + hdr, n);
+                if (tid == 0) write_header(dst + zero_here(), hdr, false, (n + hdr) | zero_here(), n | zero_here());
             }
             __syncthreads();  // the bitmap region becomes s_in / s_l8
         }
@@ -718,18 +745,16 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 if (tid == 0) s_misc[2] = 0xFFFFFFFFu;
                 __syncthreads();
                 if (tid < nseg) {
-                    uint32_t idx = I0, bb = B0, j = 0;
-                    for (uint64_t t = bits; t; t &= t - 1, j++) {
-                        const uint32_t p = s0 + (uint32_t)__builtin_ctzll(t);
-                        const uint32_t sw = (j >> 4) == 0 ? szc[0] : (j >> 4) == 1 ? szc[1] : (j >> 4) == 2 ? szc[2] : szc[3];
-                        const uint32_t sz = ((sw >> (2 * (j & 15))) & 3u) + 1u;
-                        if (idx && idx % 31u == 0 && p < P && p > 3u * (n >> 2)) {
-                            const uint32_t op = 4u * (idx / 31u) + bb;
+                    // the segment's control-word items (global item index a multiple of 31): the
+                    // r-th item sits at the r-th set bit of bits, after B0 + r + (its code sum) bytes
+                    for (uint32_t idx = (I0 + 30u) / 31u * 31u; idx < I0 + items; idx += 31u) {
+                        if (!idx) continue;
+                        const uint32_t r = idx - I0, p = s0 + select64(bits, r);
+                        if (p < P && p > 3u * (n >> 2)) {
+                            const uint32_t op = 4u * (idx / 31u) + B0 + r + fields2_prefix(szc, r);
                             atomicMin(&s_misc[2], (p << 1) | (op > p - (p >> 5) ? 1u : 0u));
                             break;
                         }
-                        idx++;
-                        bb += sz;
                     }
                 }
                 __syncthreads();
@@ -739,17 +764,13 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 if (v == 0xFFFFFFFFu || !(v & 1u)) continue;  // not decided by the prefix: pass 1
                 bail = 1;
             } else if (tid < nseg) {  // quicklz.c:216-219: at each new control word inside the main loop
-                uint32_t idx = I0, bb = B0, j = 0;
-                for (uint64_t t = bits; t; t &= t - 1, j++) {
-                    const uint32_t p = s0 + (uint32_t)__builtin_ctzll(t);
-                    const uint32_t sw = (j >> 4) == 0 ? szc[0] : (j >> 4) == 1 ? szc[1] : (j >> 4) == 2 ? szc[2] : szc[3];
-                    const uint32_t sz = ((sw >> (2 * (j & 15))) & 3u) + 1u;
-                    if (idx && idx % 31u == 0 && p < P) {
-                        const uint32_t op = 4u * (idx / 31u) + bb;
-                        if (p > 3u * (n >> 2) && op > p - (p >> 5)) bail = 1;
+                for (uint32_t idx = (I0 + 30u) / 31u * 31u; idx < I0 + items; idx += 31u) {
+                    if (!idx) continue;
+                    const uint32_t r = idx - I0, p = s0 + select64(bits, r);
+                    if (p < P && p > 3u * (n >> 2)) {
+                        const uint32_t op = 4u * (idx / 31u) + B0 + r + fields2_prefix(szc, r);
+                        if (op > p - (p >> 5)) bail = 1;
                     }
-                    idx++;
-                    bb += sz;
                 }
             }
             bail = __syncthreads_or(bail);
@@ -767,7 +788,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 } else {
                     for (uint32_t o = tid; o < n; o += T) dst[hdr + o] = s_in[o];
                 }
-                if (tid == 0) write_header(dst, hdr, false, n + hdr, n);
+                if (tid == 0) write_header(dst + zero_here(), hdr, false, (n + hdr) | zero_here(), n | zero_here());
                 csz = n + hdr;
             } else {
                 const uint32_t ncw = (Itot + 30) / 31;
@@ -806,7 +827,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     for (uint32_t o = core + tid; o < 9; o += T) dst[hdr + o] = 0;
                     core = 9;
                 }
-                if (tid == 0) write_header(dst, hdr, true, core + hdr, n);
+                if (tid == 0) write_header(dst + zero_here(), hdr, true, core + hdr, n);
                 csz = core + hdr;
             }
             break;
