@@ -162,6 +162,9 @@ constexpr uint32_t kEncGroups = 256;  // bucket groups (hash >> 4), 16 buckets e
 // 3/4 of the input + kPrefixMargin first.  On the c3 noisy blocks (40-45 % random bytes) 256 of
 // the 263 in 387 that end stored bail out at that first test, within 53 B of 3/4 of the input
 // (instrumented oracle), and D < 28 % flags them with 3 false positives.
+#ifndef QLZX_ENC_CAND_LDS
+#define QLZX_ENC_CAND_LDS 1
+#endif
 #ifndef QLZX_ENC_PREFIX
 #define QLZX_ENC_PREFIX 1
 #endif
@@ -552,6 +555,29 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 // Longest wins, ties to the larger position (quicklz.c:344): scanning from
                 // the most recent, a candidate must be strictly longer, and a match of the
                 // full extension limit ends the scan.
+#if QLZX_ENC_CAND_LDS
+                // The candidates of the wave's 64 consecutive sorted indices are the 16 entries
+                // before the first and the wave's own: each list entry is loaded from global
+                // memory once per wave-iteration into an 80-word LDS stage (s_scr is free between
+                // the sort and the parse) and the 16 candidate reads per position are LDS reads
+                // of consecutive words, not 16 global loads.
+                static_assert(C::SCR >= 80 * W, "candidate stage");
+                uint32_t *stg = s_scr + wave * 80;
+                for (uint32_t t0 = tid - lane; t0 < P; t0 += T) {  // wave-uniform
+                    const uint32_t t = t0 + lane;
+                    const bool act = t < P;
+                    const uint32_t self = act ? gl[t] : 0u;
+                    const uint32_t halo = (lane < 16 && t0 + lane >= 16) ? gl[t0 + lane - 16] : 0u;
+                    stg[16 + lane] = self;
+                    if (lane < 16) stg[lane] = halo;
+                    if (!act) continue;
+                    const uint32_t p = self & 0xFFFFu, fh = self >> 16;
+                    const uint32_t rm = (t - (uint32_t)bst[hash12(fetch24(s_in, p))]) & 255u;
+                    const uint32_t d = rm < 16u ? rm : 16u;
+                    uint32_t cand[16];  // most recent first
+#pragma unroll
+                    for (uint32_t k = 0; k < 16; k++) cand[k] = stg[k < d ? 15u + lane - k : 16u + lane];
+#else
                 for (uint32_t t = tid; t < P; t += T) {
                     const uint32_t self = gl[t], p = self & 0xFFFFu, fh = self >> 16;
                     const uint32_t rm = (t - (uint32_t)bst[hash12(fetch24(s_in, p))]) & 255u;
@@ -559,6 +585,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     uint32_t cand[16];  // most recent first; all 16 loads in flight at once
 #pragma unroll
                     for (uint32_t k = 0; k < 16; k++) cand[k] = gl[k < d ? t - 1 - k : t];
+#endif
                     const uint32_t limit = min(255u, n - 4u - p);  // quicklz.c:310
                     // First pass: bytes 3..6 of every candidate against this position's, all 16
                     // LDS reads independent.  A mismatch there gives the exact length; the
@@ -584,7 +611,11 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     while (longm && best < limit) {
                         const uint32_t k = (uint32_t)__builtin_ctz(longm);
                         longm &= longm - 1u;
+#if QLZX_ENC_CAND_LDS
+                        const uint32_t q = stg[15u + lane - k] & 0xFFFFu;
+#else
                         const uint32_t q = gl[t - 1 - k] & 0xFFFFu;
+#endif
                         uint32_t m = 7;
                         for (;;) {
                             const uint32_t x = ld32u(s_in, q + m) ^ ld32u(s_in, p + m);
