@@ -162,6 +162,9 @@ constexpr uint32_t kEncGroups = 256;  // bucket groups (hash >> 4), 16 buckets e
 // 3/4 of the input + kPrefixMargin first.  On the c3 noisy blocks (40-45 % random bytes) 256 of
 // the 263 in 387 that end stored bail out at that first test, within 53 B of 3/4 of the input
 // (instrumented oracle), and D < 28 % flags them with 3 false positives.
+#ifndef QLZX_ENC_SPEC_COPY
+#define QLZX_ENC_SPEC_COPY 1
+#endif
 #ifndef QLZX_ENC_CAND_LDS
 #define QLZX_ENC_CAND_LDS 1
 #endif
@@ -416,14 +419,15 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             for (uint32_t k = tid * 4; k < BMW; k += T * 4) *(uint4 *)(bm + k) = make_uint4(z0, z0, z0, z0);
             __syncthreads();
             const uint32_t ny = n - 2;  // positions holding a whole 3-gram
-            auto load20 = [&](uint32_t y0, uint32_t w[5]) {
-                if (y0 + 20 <= n) {
+            auto load20 = [&](uint32_t y0, uint32_t w[6]) {  // w[5] only with QLZX_ENC_SPEC_COPY
+                if (y0 + 24 <= n) {
                     const uint4 v = *(const uint4 *)(src + y0);
                     w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
                     w[4] = *(const uint32_t *)(src + y0 + 16);
+                    if (QLZX_ENC_SPEC_COPY) w[5] = *(const uint32_t *)(src + y0 + 20);
                 } else {
 #pragma unroll
-                    for (int j = 0; j < 5; j++) {
+                    for (int j = 0; j < (QLZX_ENC_SPEC_COPY ? 6 : 5); j++) {
                         uint32_t x = 0;
                         for (int k = 0; k < 4; k++) {
                             const uint32_t o = y0 + 4 * j + k;
@@ -433,7 +437,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     }
                 }
             };
-            auto mark16 = [&](uint32_t y0, const uint32_t w[5]) {
+            auto mark16 = [&](uint32_t y0, const uint32_t w[6]) {
                 // fully unrolled (w[] indices static: a partial unroll turned every w[j / 4] into a
                 // select chain); the per-position range test only in the block's last piece
                 if (y0 + 16 <= ny) {
@@ -454,14 +458,31 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     }
                 }
             };
+            // Speculative stored copy: most blocks the proof sees end stored, and the proof already
+            // has their bytes in registers, so the 16-B destination chunks [16, a1) of the stored
+            // value (header + input: chunk o holds input bytes o - 9 ..) go out now, each from the
+            // window of the step 16 bytes before it.  A block that is not stored overwrites them
+            // (its output is shorter; dst capacity is >= n + 400).
+            const bool spec = QLZX_ENC_SPEC_COPY && hdr == 9 && (((uintptr_t)dst) & 15u) == 0;
+            const uint32_t sa1 = (n + hdr) & ~15u;
+            auto spec16 = [&](uint32_t y0, const uint32_t w[6]) {
+                if (spec && y0 + 32 <= sa1)
+                    *(uint4 *)(dst + y0 + 16) = make_uint4(
+                        __builtin_amdgcn_alignbyte(w[2], w[1], 3), __builtin_amdgcn_alignbyte(w[3], w[2], 3),
+                        __builtin_amdgcn_alignbyte(w[4], w[3], 3), __builtin_amdgcn_alignbyte(w[5], w[4], 3));
+            };
             // two 16-position steps per iteration, both loads in flight before either is hashed
             for (uint32_t y0 = tid * 16; y0 < ny; y0 += 2 * T * 16) {
-                uint32_t wa[5], wb[5] = {0, 0, 0, 0, 0};
+                uint32_t wa[6] = {0, 0, 0, 0, 0, 0}, wb[6] = {0, 0, 0, 0, 0, 0};
                 const uint32_t y1 = y0 + T * 16;
                 load20(y0, wa);
                 if (y1 < ny) load20(y1, wb);
                 mark16(y0, wa);
-                if (y1 < ny) mark16(y1, wb);
+                spec16(y0, wa);
+                if (y1 < ny) {
+                    mark16(y1, wb);
+                    spec16(y1, wb);
+                }
             }
             __syncthreads();
             uint32_t ones = 0;
@@ -483,7 +504,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     // (one dependent load per step made the copy latency-bound: 70 K cycles)
                     const uint32_t tot = n + hdr, a0 = (hdr + 15u) & ~15u, a1 = tot & ~15u;
                     constexpr uint32_t K = 4;
-                    for (uint32_t o0 = a0 + tid * 16; o0 < a1; o0 += T * 16 * K) {
+                    for (uint32_t o0 = a0 + tid * 16; o0 < (spec ? a0 : a1); o0 += T * 16 * K) {  // spec: done
                         uint4 v[K];
 #pragma unroll
                         for (uint32_t k = 0; k < K; k++) {
