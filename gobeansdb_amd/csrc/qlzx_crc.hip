@@ -155,13 +155,15 @@ __device__ uint32_t wave_crc(const uint32_t *lds, const uint8_t *p, uint64_t len
 // lookup per byte either way).  mul = the g_crc_mul tables (LDS or global).  The two 32-B halves
 // of a piece run as two independent chains (the lookups are a dependent-latency chain), joined
 // through g_crc_mul32 (global).
-template <uint32_t R>
+// S4: tab holds the slicing-by-4 tables instead (g_crc_slice8[0..1023], 4 KiB, no copies): four
+// independent lookups per dword instead of a chain of four, one VALU less per byte, more conflicts.
+template <uint32_t R, bool S4 = false>
 __device__ uint32_t wave_crc_rep(const uint32_t *tab, const uint32_t *mul, const uint8_t *p, uint64_t len,
                                  uint32_t init, uint32_t lane) {
-    const uint32_t *tr = tab + (lane & (R - 1));
+    const uint32_t *tr = S4 ? tab : tab + (lane & (R - 1));
     if (len < 4) {
         uint32_t c = init;
-        for (uint32_t b = 0; b < len; b++) c = tr[((c ^ p[b]) & 0xffu) * R] ^ (c >> 8);
+        for (uint32_t b = 0; b < len; b++) c = tr[((c ^ p[b]) & 0xffu) * (S4 ? 1u : R)] ^ (c >> 8);
         return c;
     }
     const uint32_t m = (uint32_t)((uintptr_t)p & 3u);
@@ -206,10 +208,15 @@ __device__ uint32_t wave_crc_rep(const uint32_t *tab, const uint32_t *mul, const
         for (int k = 0; k < 8; k++) {
             c ^= w[k];
             d ^= w[k + 8];
+            if constexpr (S4) {
+                c = tr[768 + (c & 0xffu)] ^ tr[512 + ((c >> 8) & 0xffu)] ^ tr[256 + ((c >> 16) & 0xffu)] ^ tr[c >> 24];
+                d = tr[768 + (d & 0xffu)] ^ tr[512 + ((d >> 8) & 0xffu)] ^ tr[256 + ((d >> 16) & 0xffu)] ^ tr[d >> 24];
+            } else {
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-                c = tr[(c & 0xffu) * R] ^ (c >> 8);
-                d = tr[(d & 0xffu) * R] ^ (d >> 8);
+                for (int b = 0; b < 4; b++) {
+                    c = tr[(c & 0xffu) * R] ^ (c >> 8);
+                    d = tr[(d & 0xffu) * R] ^ (d >> 8);
+                }
             }
         }
         c = crc_mul_tab(g_crc_mul32, c) ^ d;

@@ -261,8 +261,12 @@ __device__ __forceinline__ void dec_bytes_block(K2bLds<W, MR> &L, const uint8_t 
 }
 
 // CRC: the record CRC (store/datafile.go:161-168) is verified first, over all src_len bytes from
-// crc_state (or ~0), with the byte table four times over in the window (wave_crc_rep<4>) and the
-// g_crc_mul tables read from global memory; a mismatch sets QLZX_E_CRC and nothing is decoded.
+// crc_state (or ~0), with the slicing-by-4 tables in the 4 KiB window (wave_crc_rep<4, true>; the
+// byte table four times over, QLZX_K2_CRC_S4=0, measured ~1 % slower on c2 + CRC) and the g_crc_mul
+// tables read from global memory; a mismatch sets QLZX_E_CRC and nothing is decoded.
+#ifndef QLZX_K2_CRC_S4
+#define QLZX_K2_CRC_S4 1
+#endif
 template <uint32_t W, uint32_t MR, bool CRC>
 __global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                                                   uint32_t first, uint32_t count, const BlkInfo *info,
@@ -277,13 +281,18 @@ __global__ void __launch_bounds__(64) k_dec_bytes(qlzx_blocks b, uint32_t *dsize
         static_assert(W >= 4096, "the 4-fold CRC table fills 4 KiB of the window");
         const uint32_t lane = threadIdx.x;
         uint32_t *tab = (uint32_t *)L.win;
+#if QLZX_K2_CRC_S4
+        for (uint32_t e = lane * 4; e < 1024; e += 256)
+            *(uint4 *)(tab + e) = *(const uint4 *)(g_crc_slice8 + e);
+#else
         for (uint32_t e = lane; e < 256; e += 64) {
             const uint32_t v = g_crc_table[e];
             *(uint4 *)(tab + 4 * e) = make_uint4(v, v, v, v);
         }
+#endif
         __syncthreads();
-        const uint32_t c = ~wave_crc_rep<4>(tab, g_crc_mul, b.src + b.src_off[i], b.src_len[i],
-                                            crc_state ? crc_state[i] : 0xffffffffu, lane);
+        const uint32_t c = ~wave_crc_rep<4, QLZX_K2_CRC_S4>(tab, g_crc_mul, b.src + b.src_off[i], b.src_len[i],
+                                                             crc_state ? crc_state[i] : 0xffffffffu, lane);
         __syncthreads();  // the window is the decode's again
         if (lane == 0 && crc_out) crc_out[i] = c;
         if (crc_expect && c != crc_expect[i]) {
