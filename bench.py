@@ -346,6 +346,8 @@ def main():
         if mixed is not None:
             rec["mixed"] = {k: mixed[k] for k in ("metric", "value", "unit", "scaling", "rounds_per_gpu", "wall_s",
                                                   "config", "roofline")}
+            if world == 1 and not args.no_cpu:  # CPU leg at N = 1 only, like the other legs
+                rec["mixed"]["cpu_baseline"] = cpu_baseline_mixed(max(2.0, args.cpu_seconds / 2))
         print(json.dumps(rec), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
@@ -618,6 +620,54 @@ def cpu_baseline(kind: str, bs: int, seconds: float, mode: str = "decompress", g
             "cgo_faithful": round(cgo, 3),
             "cgo_faithful_what": "per call: output + scratch malloc/free as quicklz/cquicklz.go:24-49",
             "compress_parity": parity}
+
+
+def cpu_baseline_mixed(seconds: float):
+    """c5's CPU leg: the reference qlz_decompress (oracle/_ref; else the C restatement) on the
+    host cores over a bounded sample of the same value mix (log-uniform 4-64 KiB, 70 % text /
+    30 % image-like, as tools/bench_c5.py draws them), GiB/s of output."""
+    from oracle import oracle as O
+    threads, nproc, model = host_cpus()
+    L = O.lib()
+    Q = O.ref_if_built()
+    rng = np.random.default_rng(SEED)
+    nblk = 2048
+    sizes = [int(np.exp(rng.uniform(np.log(4096), np.log(65536)))) for _ in range(nblk)]
+    is_text = rng.random(nblk) < 0.7
+    plain = [(O.gen_text if t else O.gen_image)(SEED, i, n) for i, (t, n) in enumerate(zip(is_text, sizes))]
+    comp = [O.compress(p_) for p_ in plain]
+    off_s, tot_s = _pack(comp)
+    off_d, tot_d = _pack(plain)
+    srcb = np.zeros(tot_s, np.uint8)
+    for o, c in zip(off_s, comp):
+        srcb[int(o): int(o) + len(c)] = np.frombuffer(c, np.uint8)
+    lens = np.asarray([len(c) for c in comp], np.uint32)
+    dst = np.zeros(tot_d, np.uint8)
+    out_bytes = sum(sizes)
+    fn = ctypes.cast(Q.qlz_decompress, ctypes.c_void_p).value if Q else None
+
+    def run(nthr, secs):
+        reps, ns = 0, 0.0
+        t_end = time.time() + secs
+        while time.time() < t_end or reps == 0:
+            if Q is not None:
+                ns += L.orc_bench_ref(fn, srcb.ctypes.data, off_s.ctypes.data, lens.ctypes.data,
+                                      dst.ctypes.data, off_d.ctypes.data, nblk, nthr, 0)
+            else:
+                ns += L.orc_bench_decompress(srcb.ctypes.data, off_s.ctypes.data, lens.ctypes.data,
+                                             dst.ctypes.data, off_d.ctypes.data, nblk, nthr, 0)
+            reps += 1
+        return reps * out_bytes / (ns * 1e-9) / 2**30, reps
+
+    gibs, reps = run(threads, seconds)
+    if not all(dst[int(o): int(o) + len(p_)].tobytes() == p_ for o, p_ in zip(off_d[:16], plain[:16])):
+        raise RuntimeError("mixed decompress baseline produced wrong bytes")
+    one, _ = run(1, max(2.0, seconds / 5))
+    what = REF_WHAT.format(fn="qlz_decompress") if Q is not None else "oracle/qlz_oracle.c orc_decompress"
+    return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "reference" if Q else "port",
+            "sample": f"{reps} passes over {nblk} log-uniform 4-64 KiB values (70 % text / 30 % image-like, "
+                      f"{out_bytes / 2**20:.1f} MiB out), {what}, {threads} threads, GiB/s of output; no CRC",
+            "threads": threads, "nproc": nproc, "cpu_model": model, "one_core": round(one, 3)}
 
 
 def _pack(blocks):
