@@ -17,9 +17,9 @@ LIB_PATH = os.environ.get("QLZX_LIB", os.path.join(HERE, "libqlzx.so"))
 HEADER = os.path.join(ROOT, "include", "qlzx.h")
 
 # enum qlzx_status
-OK, E_SIZE_COMPRESSED, E_CORRUPT, E_LEVEL, E_DST_CAP, E_CRC, E_HEADER, E_EMPTY, E_TOO_LARGE, E_MAX_DSIZE = range(10)
+OK, E_SIZE_COMPRESSED, E_CORRUPT, E_LEVEL, E_DST_CAP, E_CRC, E_HEADER, E_EMPTY, E_TOO_LARGE, E_MAX_DSIZE, E_RUNTIME = range(11)
 STATUS_NAMES = ["OK", "E_SIZE_COMPRESSED", "E_CORRUPT", "E_LEVEL", "E_DST_CAP", "E_CRC",
-                "E_HEADER", "E_EMPTY", "E_TOO_LARGE", "E_MAX_DSIZE"]
+                "E_HEADER", "E_EMPTY", "E_TOO_LARGE", "E_MAX_DSIZE", "E_RUNTIME"]
 
 
 F_GO_COMPAT = 1

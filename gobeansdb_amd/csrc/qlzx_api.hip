@@ -51,6 +51,8 @@ constexpr uint32_t kMaxLaneSlabs = 4096;  // concurrent lane encoders for the ge
 
 }  // namespace
 
+#include "qlzx_service.hip"
+
 #ifdef QLZX_PROFILE
 namespace qlzx {
 __device__ unsigned long long *g_prof = nullptr;
@@ -290,11 +292,7 @@ int qlzx_vhash_batch(const uint8_t *src, const uint64_t *off, const uint32_t *le
  * buffers are touched only by host memcpy. */
 namespace {
 
-// Set by an atexit handler registered at the first context init, i.e. after the HIP runtime
-// registered its own teardown (atexit runs in reverse order): contexts destroyed after that
-// (threads exiting during process exit) skip the HIP frees.
-std::atomic<bool> g_hip_down{false};
-void mark_hip_down() { g_hip_down.store(true); }
+using qlzx::g_hip_down;
 
 struct Meta {  // one-block batch descriptors, device side
     uint64_t src_off, dst_off;
@@ -319,11 +317,18 @@ struct Ctx {
         if (ok) return 0;
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(QLZX_R_NO_DEVICE, "no HIP device");
-        static std::once_flag once;
-        std::call_once(once, [] { std::atexit(mark_hip_down); });
+        qlzx::note_hip_up();
         HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         ok = true;
         return 0;
+    }
+    // Buffers of a call above kCtxKeep are released after it: a thread keeps at most kCtxKeep
+    // of each (the single-call sizes the service does not take are the rare large values).
+    static constexpr size_t kCtxKeep = 8u << 20;
+    void trim() {
+        if (g_hip_down.load()) return;
+        if (d_cap > kCtxKeep) (void)hipFree(d_buf), d_buf = nullptr, d_cap = 0;
+        if (h_cap > kCtxKeep) (void)hipHostFree(h_buf), h_buf = nullptr, h_cap = 0;
     }
     int reserve(size_t dev_bytes, size_t host_bytes) {
         if (dev_bytes > d_cap) {
@@ -370,6 +375,27 @@ thread_local int t_last_status = QLZX_OK;
 // *csize (0 with t_last_status != OK when the kernel rejects the block).
 int compress1(const void *source, char *destination, size_t size, uint32_t flags, size_t *csize) {
     *csize = 0;
+    t_last_status = QLZX_E_RUNTIME;  // replaced below; never left over from an earlier call
+    if (flags == 0 && size <= qlzx::kSvcMaxLen) {  // the request path (qlzx_service.hip)
+        Service *S = service();
+        if (!S) return QLZX_R_NO_DEVICE;
+        const uint32_t b = S->take_slot();
+        memcpy(S->in(b), source, size);
+        qlzx::SvcReq r{};
+        r.slot = b, r.len = (uint32_t)size, r.cap = (uint32_t)size + 400;
+        const int rc = S->run(qlzx::kSvcCompress, r);
+        const qlzx::SvcDone d = *(const qlzx::SvcDone *)(S->h_done + b);
+        if (rc == QLZX_R_OK) {
+            t_last_status = d.status;
+            if (d.status == QLZX_OK && (d.out == 0 || d.out > size + 400)) {
+                S->give_slot(b);
+                return fail(QLZX_R_HIP, "compress1: bad result size");
+            }
+            if (d.status == QLZX_OK) memcpy(destination, S->out(b), d.out), *csize = d.out;
+        }
+        S->give_slot(b);
+        return rc;
+    }
     Ctx &c = t_ctx;
     if (int r = c.init()) return r;
     const bool l1 = (flags & QLZX_F_LEVEL1) != 0;
@@ -403,6 +429,7 @@ int compress1(const void *source, char *destination, size_t size, uint32_t flags
     if (m->out_size == 0 || m->out_size > size + 400) return fail(QLZX_R_HIP, "compress1: bad result size");
     memcpy(destination, h_data, m->out_size);
     *csize = m->out_size;
+    c.trim();
     return QLZX_R_OK;
 }
 
@@ -411,9 +438,26 @@ int compress1(const void *source, char *destination, size_t size, uint32_t flags
 int decompress1(const char *source, void *destination, size_t *dsize_out) {
     *dsize_out = 0;
     const size_t csize = qlz_size_compressed(source), dsize = qlz_size_decompressed(source);
+    t_last_status = QLZX_E_RUNTIME;  // replaced below; never left over from an earlier call
     if (csize < 3) {
         t_last_status = QLZX_E_HEADER;
         return QLZX_R_OK;
+    }
+    if (dsize <= qlzx::kSvcMaxLen && csize <= qlzx::kSoloMaxCsize) {  // the request path
+        Service *S = service();
+        if (!S) return QLZX_R_NO_DEVICE;
+        const uint32_t b = S->take_slot();
+        memcpy(S->in(b), source, csize);
+        qlzx::SvcReq r{};
+        r.slot = b, r.len = (uint32_t)csize, r.cap = (uint32_t)dsize;
+        const int rc = S->run(qlzx::kSvcDecode, r);
+        const qlzx::SvcDone d = *(const qlzx::SvcDone *)(S->h_done + b);
+        if (rc == QLZX_R_OK) {
+            t_last_status = d.status;
+            if (d.status == QLZX_OK) memcpy(destination, S->out(b), d.out), *dsize_out = d.out;
+        }
+        S->give_slot(b);
+        return rc;
     }
     Ctx &c = t_ctx;
     if (int r = c.init()) return r;
@@ -446,9 +490,11 @@ int decompress1(const char *source, void *destination, size_t *dsize_out) {
     if (dsize) HIP_OK(hipMemcpyAsync(h_data, d_dst, dsize, hipMemcpyDeviceToHost, c.s));
     HIP_OK(hipStreamSynchronize(c.s));
     t_last_status = m->status;
-    if (m->status != QLZX_OK) return QLZX_R_OK;
-    memcpy(destination, h_data, dsize);
-    *dsize_out = m->out_size;
+    if (m->status == QLZX_OK) {
+        memcpy(destination, h_data, dsize);
+        *dsize_out = m->out_size;
+    }
+    c.trim();
     return QLZX_R_OK;
 }
 
@@ -467,6 +513,7 @@ size_t qlz_compress(const void *source, char *destination, size_t size, char *sc
 }
 
 size_t qlzx_compress1(const void *source, char *destination, size_t size, uint32_t flags) {
+    t_last_status = QLZX_E_RUNTIME;
     if (size == 0 || size > 0xffffffffull - 400) {  // quicklz.c:705-706
         t_last_status = size ? QLZX_E_TOO_LARGE : QLZX_E_EMPTY;
         return 0;
@@ -483,6 +530,7 @@ size_t qlz_decompress(const char *source, void *destination, char *scratch_decom
 }
 
 size_t qlzx_go_decompress1(const char *source, size_t source_len, void *destination, size_t dst_cap) {
+    t_last_status = QLZX_E_RUNTIME;  // replaced below; never left over from an earlier call
     if (!source || source_len == 0) {
         t_last_status = QLZX_E_HEADER;
         return QLZX_GO_ERROR;
@@ -528,6 +576,19 @@ size_t qlzx_go_decompress1(const char *source, size_t source_len, void *destinat
 
 uint32_t crc32_write(uint32_t crc, unsigned char *buf, int len) {
     if (len <= 0) return crc;  // store/crc32.go:65 loops zero times
+    if ((size_t)len <= qlzx::kSvcIn - 64) {  // the request path (qlzx_service.hip)
+        Service *S = service();
+        if (!S) die("crc32_write");
+        const uint32_t b = S->take_slot();
+        memcpy(S->in(b), buf, (size_t)len);
+        qlzx::SvcReq r{};
+        r.slot = b, r.len = (uint32_t)len, r.arg = crc;
+        const int rc = S->run(qlzx::kSvcCrc, r);
+        const uint32_t v = ((const qlzx::SvcDone *)S->h_done)[b].crc;
+        S->give_slot(b);
+        if (rc != QLZX_R_OK) die("crc32_write");
+        return v;
+    }
     Ctx &c = t_ctx;
     if (c.init()) die("crc32_write");
     const size_t src_b = align_up((size_t)len, 256);
@@ -549,7 +610,9 @@ uint32_t crc32_write(uint32_t crc, unsigned char *buf, int len) {
         fail(QLZX_R_HIP, "crc32_write", e);
         die("crc32_write");
     }
-    return m->crc_out;
+    const uint32_t v = m->crc_out;
+    c.trim();
+    return v;
 }
 
 }  // extern "C"

@@ -117,10 +117,11 @@ __device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t *wsum, uint3
     } while (0)
 #endif
 
-__global__ void __launch_bounds__(kSoloWG) k_dec_solo(const uint8_t *src, uint32_t len, uint8_t *dst,
-                                                     uint32_t dst_cap, uint32_t max_dsize, GroupRec *recs,
-                                                     int32_t *status, uint32_t *dsize_out) {
-    __shared__ __attribute__((aligned(16))) SoloLds L;
+// The whole block by one 1024-thread workgroup; *status / *dsize_out are written by thread 0
+// (global or LDS words).  Every return is workgroup-uniform.
+__device__ __forceinline__ void solo_decode(SoloLds &L, const uint8_t *src, uint32_t len, uint8_t *dst,
+                                            uint32_t dst_cap, uint32_t max_dsize, GroupRec *recs, int32_t *status,
+                                            uint32_t *dsize_out) {
     const uint32_t tid = threadIdx.x;
     SOLO_T0
     uint32_t kind, csize = 0, dsize = 0, hdr = 0;
@@ -416,6 +417,13 @@ __global__ void __launch_bounds__(kSoloWG) k_dec_solo(const uint8_t *src, uint32
     }
     if (tid == 0) *status = QLZX_OK, *dsize_out = dsize;
     SOLO_STAMP(7);
+}
+
+__global__ void __launch_bounds__(kSoloWG) k_dec_solo(const uint8_t *src, uint32_t len, uint8_t *dst,
+                                                     uint32_t dst_cap, uint32_t max_dsize, GroupRec *recs,
+                                                     int32_t *status, uint32_t *dsize_out) {
+    __shared__ __attribute__((aligned(16))) SoloLds L;
+    solo_decode(L, src, len, dst, dst_cap, max_dsize, recs, status, dsize_out);
 }
 
 // One block (len stream bytes at src, dsize <= QLZX_FAST_MAX_DSIZE, len <= kSoloMaxCsize):

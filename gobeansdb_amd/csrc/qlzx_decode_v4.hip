@@ -1,0 +1,397 @@
+// qlzx_decode_v4.hip -- round-4 batch decoder pair (dsize <= QLZX_FAST_MAX_DSIZE):
+//
+// K1 k_dec_parse4  one LANE per block: the serial control-word chain of quicklz.c:513-671,
+//     one item STEP at a time (a literal run and the match that ends it, or a control word),
+//     reading only control words and the first byte of each match token.  The remaining
+//     control bits are kept with their sentinel (cwr; 1 = group exhausted), so the item index
+//     is clz(cwr) and a literal run is ctz(cwr): no per-item counters, no multi-match step.
+//     Emits one GroupRec {ip, cw, a, b} per control word (a, b: bit-planes of token bytes - 1).
+//
+// K2 k_dec_chunk4  one WAVE per block, 64 items per batch and 256 output bytes per chunk:
+//     * ITEM PHASE: token position from the GroupRec, branch-free token decode, DPP scan of the
+//       output lengths; item i leaves ONE u32 key (d << 16 | off) in a 512-entry marker ring
+//       at slot d (off = 0 for a literal, whose byte also goes to the output window);
+//     * CHUNK PHASE: lane l owns bytes c + 4l .. c + 4l + 3.  The keys grow with d, so the
+//       forward fill of "the item covering byte p" is a max-scan (in-lane max + DPP max across
+//       lanes + the previous chunk's carry) and the source is s = p - (key & 0xffff) for match
+//       and literal bytes alike.  In-chunk sources are chased by pointer jumping over the
+//       chunk's own marker slots (free once read), then every byte is gathered from the 4 KiB
+//       LDS window (or, when older than the window, from the block's output in HBM).
+//     The batch loop is unrolled by two with two register sets for the prefetched GroupRec and
+//     token dword, so no prefetched register is copied (and waited for) at a batch boundary.
+//
+// Checks C1-C5 are applied exactly as by the oracle (oracle/qlz_oracle.c:180-231).
+namespace qlzx {
+
+// ------------------------------------------------------------------------------- K1 ----
+__global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
+                                                     int32_t *status, uint32_t first, uint32_t count, BlkInfo *info,
+                                                     GroupRec *recs, uint32_t gmax, const uint32_t *order,
+                                                     uint32_t max_dsize) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG / 64) * kRingWave];
+    const uint32_t lane = threadIdx.x & 63;
+    uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWave;
+    const uint32_t lin = blockIdx.x * kParseWG + threadIdx.x;
+    const bool inrange = lin < count;
+    const uint32_t i = inrange ? (order ? order[lin] : first + lin) : first;
+
+    int st = QLZX_OK;
+    uint32_t kind = kBlkSkip, csize = 0, dsize = 0, hdr = 0, len = 0;
+    const uint8_t *src = b.src + b.src_off[i];
+    if (inrange) {
+        len = b.src_len[i];
+        st = classify_block(src, len, dst_cap ? dst_cap[i] : 0xffffffffu, max_dsize, kind, csize, dsize, hdr);
+        // a compressed stream of dsize 0 decodes to nothing: the oracle's loop never runs and C5
+        // accepts csize == hdr or the 9-byte core minimum (oracle/qlz_oracle.c:197,228)
+        if (st == QLZX_OK && kind == kBlkCompressed && dsize == 0) {
+            st = (csize == hdr || csize == hdr + 9) ? QLZX_OK : QLZX_E_CORRUPT;
+            kind = kBlkSkip;
+        }
+    }
+    const uintptr_t a0 = (uintptr_t)src;
+    const uint8_t *gbase = (const uint8_t *)(a0 & ~(uintptr_t)15);
+    const uint32_t shift = (uint32_t)(a0 & 15);
+    const uint32_t span = (st == QLZX_OK && kind == kBlkCompressed) ? csize : 0;
+    const uint32_t last16 = span ? (span + shift - 1) >> 4 : 0;
+    const uint32_t last_round = span ? (span + shift - 1) / kRoundBytes : 0;
+    bool stream = inrange && span > 0;
+    const bool parsing = stream;
+
+    // parse state: ip = next stream byte; cwr = control bits not consumed yet, sentinel
+    // included (1: the group is exhausted, the next step reads a control word)
+    uint32_t ip = hdr, g = 0, cwr = 1, cwg = 0, ra = 0, rb = 0, rec_ip = 0;
+    GroupRec *myrec = recs + (size_t)(inrange ? lin : 0) * gmax;
+    bool done_parse = !parsing;
+
+    PROF_DECL
+    const uint8_t *dummy = (const uint8_t *)(((uintptr_t)b.src) & ~(uintptr_t)15);
+    ring_issue(ring, gbase, dummy, 0, last16, stream);
+    ring_issue(ring, gbase, dummy, 1, last16, stream && last_round >= 1);
+    ring_issue(ring, gbase, dummy, 2, last16, stream && last_round >= 2);
+    for (uint32_t r = 0;; r++) {
+        if (__ballot(stream && r <= last_round) == 0) break;
+        PROF_MARK(0);
+#if QLZX_K1_ROUND == 64
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+#else
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#endif
+        PROF_MARK(1);
+        const bool act = stream && r <= last_round;
+        const uint32_t lim = (r + 1) * kRoundBytes - shift;  // stream bytes below lim have landed
+        bool go = act && !done_parse;
+        while (__ballot(go)) {
+#ifdef QLZX_PROFILE
+            _pacc[5] += 1;
+            if (go) _pacc[6] += 1;
+#endif
+            const bool gb = cwr == 1;
+            const uint32_t rem = csize - ip;
+            uint32_t run = __builtin_ctz(cwr);  // literals before the next match (or the sentinel)
+            run = run < rem ? run : rem;
+            const uint32_t q = ip + run;        // control word (gb) or the match token
+            const uint32_t rest = cwr >> run;
+            const bool hasm = !gb & (rest != 1u) & ((rest & 1u) != 0) & (q < csize);
+            const bool end = ip + (gb ? 4u : 1u) > csize;
+            const uint32_t need = gb ? 4u : 1u;
+            const bool landed = q + need <= lim;
+            const bool stepping = go & !end & ((gb | hasm) ? landed : true);
+            const uint32_t w = ring_rd32(ring, q + shift, lane);
+            const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
+            const uint32_t e = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);  // token bytes - 1
+            const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) | (hasm & (q + e + 1 > csize)));
+            if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, cwg, ra, rb};
+            st = bad ? QLZX_E_CORRUPT : st;
+            const bool adv = stepping & !bad;
+            const uint32_t kb = hasm ? 1u << (__builtin_clz(cwr) + run) : 0u;  // item index clz(cwr) + run
+            const uint32_t nip = gb ? ip + 4 : q + (hasm ? e + 1 : 0u);
+            const uint32_t ncwr = gb ? w : (rest >> (hasm ? 1 : 0));
+            const uint32_t nra = gb ? 0u : (ra | ((e & 1u) ? kb : 0u));
+            const uint32_t nrb = gb ? 0u : (rb | ((e & 2u) ? kb : 0u));
+            rec_ip = (adv & gb) ? ip : rec_ip;
+            cwg = (adv & gb) ? w : cwg;
+            g += (adv & gb) ? 1u : 0u;
+            ip = adv ? nip : ip;
+            cwr = adv ? ncwr : cwr;
+            ra = adv ? nra : ra;
+            rb = adv ? nrb : rb;
+            done_parse = done_parse | (go & (end | bad));
+            go = adv;
+        }
+        PROF_MARK(3);
+        if (done_parse) stream = false;
+        ring_issue(ring, gbase, dummy, r + 3, last16, stream && r + 3 <= last_round);
+    }
+    PROF_MARK(4);
+    if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, cwg, ra, rb};
+    PROF_FLUSH(0);
+    vm_sync();
+    if (!inrange) return;
+    if (st == QLZX_OK && kind == kBlkCompressed && (!done_parse || g == 0)) st = QLZX_E_CORRUPT;
+    BlkInfo bi{0, 0, kind, dsize};
+    if (st != QLZX_OK) {
+        bi.kind = kBlkSkip;
+        status[i] = st;
+        if (dsize_out && st != kPending) dsize_out[i] = 0;
+    } else if (kind == kBlkCompressed) {
+        bi.ngroups = g;
+        bi.nitems = (g - 1) * 31 + __builtin_clz(cwr);  // items consumed in the last group
+    } else if (kind == kBlkSkip) {  // dsize-0 compressed stream accepted above
+        status[i] = QLZX_OK;
+        if (dsize_out) dsize_out[i] = 0;
+    }
+    info[lin] = bi;
+}
+
+// ------------------------------------------------------------------------------- K2 ----
+constexpr uint32_t kV4W = 4096;   // output window (LDS ring)
+constexpr uint32_t kV4MR = 512;   // marker ring (u32 keys)
+constexpr uint32_t kV4Chunk = 256;
+
+struct K2v4Lds {
+    uint8_t win[kV4W];
+    uint32_t mk[kV4MR];
+};
+
+// Inclusive max over lanes 0..lane; DPP row shifts + row broadcasts.
+__device__ __forceinline__ uint32_t v4_incl_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+
+__device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uint8_t *dst, uint32_t csize,
+                                             const BlkInfo bi, const GroupRec *rb, int32_t *status_i,
+                                             uint32_t *dsize_i, uint32_t lane) {
+    constexpr uint32_t W = kV4W, MR = kV4MR, CH = kV4Chunk;
+    const uint32_t dsize = bi.dsize;
+    if (bi.kind == kBlkStored) {  // quicklz.c:808-811
+        const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
+        const uint8_t *s = src + hdr;
+        uint32_t p0 = 0;
+        if ((((uintptr_t)dst) & 15u) == 0) {
+            p0 = dsize & ~15u;
+            for (uint32_t p = lane * 16; p < p0; p += 1024) {
+                const uint32_t *q = (const uint32_t *)(s + p);
+                *(uint4 *)(dst + p) = make_uint4(q[0], q[1], q[2], q[3]);
+            }
+        }
+        for (uint32_t p = p0 + lane; p < dsize; p += 64) dst[p] = s[p];
+        if (lane == 0) { *status_i = QLZX_OK; if (dsize_i) *dsize_i = dsize; }
+        return;
+    }
+    *(uint4 *)(L.mk + lane * 4) = make_uint4(0, 0, 0, 0);
+    *(uint4 *)(L.mk + 256 + lane * 4) = make_uint4(0, 0, 0, 0);
+
+    const uint32_t nitems = bi.nitems;
+    const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
+    const uint32_t nb = (nitems + 63) / 64;
+    const uint32_t tail_from = dsize > QLZX_TAIL ? dsize - 1 - QLZX_TAIL : 0;  // op >= this: tail (quicklz.c:503)
+
+    auto tok_pos = [&](const GroupRec &gr, const ItemCursor &c, bool v, uint32_t &p) -> uint32_t {
+        const uint32_t low = (1u << c.k) - 1u;
+        const uint32_t pos = gr.ip + 4 + c.k + __builtin_popcount(gr.a & low) + 2 * __builtin_popcount(gr.b & low);
+        p = v ? (pos + 4 <= csize ? pos : csize - 4) : 0u;
+        return v ? (pos | (((gr.m >> c.k) & 1u) << 31)) : 0u;
+    };
+    // register sets: (posm, tok) of the batch being decoded and of the next; GroupRec of the
+    // batch after the decoded one and of the one after that
+    ItemCursor ck{lane / 31, lane % 31};
+    uint32_t posmA, tokA, posmB = 0, tokB = 0;
+    GroupRec grA, grB;
+    {
+        const bool v0 = lane < nitems;
+        const GroupRec g0 = rb[v0 ? ck.g : 0u];
+        uint32_t tp;
+        posmA = tok_pos(g0, ck, v0, tp);
+        tokA = *(const uint32_t *)(src + tp);
+        ck.next();
+        grB = rb[64 + lane < nitems ? ck.g : 0u];
+        grA = grB;
+    }
+    uint32_t D = 0, bt = 0, c = 0, cin = 0;
+    bool tail = false, complete = false, err = false;
+    uint64_t pend = 0;
+    uint32_t pd = 0, pkey = 0;
+    uint32_t plit = 0;
+
+    // one batch: decode (posm, tok), prefetch the next batch's token from gr_next into
+    // (posm_n, tok_n) and the GroupRec after it into gr_nn
+    auto batch = [&](uint32_t posm, uint32_t tok, const GroupRec &gr_next, uint32_t &posm_n, uint32_t &tok_n,
+                     GroupRec &gr_nn) __attribute__((always_inline)) {
+        const bool v = bt * 64 + lane < nitems;
+        {
+            const bool v1 = (bt + 1) * 64 + lane < nitems;
+            uint32_t tp;
+            posm_n = tok_pos(gr_next, ck, v1, tp);
+            tok_n = *(const uint32_t *)(src + tp);
+            ck.next();
+            gr_nn = rb[(bt + 2) * 64 + lane < nitems ? ck.g : 0u];
+        }
+        const bool ism = (posm >> 31) != 0;
+        const uint32_t pos = posm & 0x7fffffffu;
+        const uint32_t t = pos + 4 <= csize ? tok : tok >> (8 * (pos + 4 - csize));
+        uint32_t off, mlen, tl;
+        decode_tok_bf(t, off, mlen, tl);
+        const uint32_t len = ism ? mlen : (v ? 1u : 0u);
+        const uint32_t incl = wave_incl_scan(len);
+        const uint32_t total = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(incl, 63));
+        const uint32_t d = D + incl - len;
+        const bool live = v && d < dsize;
+        bool bad, last = false;
+        if (tail || D + total > tail_from) {
+            tl = ism ? tl : 1u;
+            const uint64_t tail_lanes = __ballot(live && !ism && d >= tail_from);
+            const uint32_t tail_lane = tail ? 0u : ff1_or(tail_lanes, 64u);  // C4: no match after it
+            tail = tail || tail_lanes != 0;
+            const bool mok = off >= 3 && off <= d && d + len + 4 <= dsize && lane < tail_lane;  // C3, C4
+            last = live && d + len == dsize;  // C5: the item completing dsize ends the stream
+            const uint32_t ip_end = pos + tl;
+            const bool eok = ip_end == csize || (ip_end < hdr + 9 && csize == hdr + 9);
+            bad = live && ((ism && !mok) || (last && !eok));
+        } else {
+            bad = ism && (off < 3 || off > d);  // C3
+        }
+        if (__ballot(bad)) {
+            err = true;
+            return;
+        }
+        complete = __ballot(last) != 0;
+        const uint32_t key = (d << 16) | (ism ? off : 0u);
+        const bool wr = live && d < c + MR;
+        if (wr) {
+            L.mk[d & (MR - 1)] = key;
+            if (!ism) L.win[d & (W - 1)] = (uint8_t)t;
+        }
+        pend = __ballot(live && !wr);
+        pd = d;
+        pkey = key;
+        plit = ism ? 0x100u : (t & 0xffu);
+        D = __builtin_amdgcn_readfirstlane(D + total);
+        bt++;
+    };
+
+    // chunk phases while every item starting below c + 256 is known; true when the block is done
+    auto chunks = [&]() __attribute__((always_inline)) -> bool {
+        while (c < dsize && (complete || D >= c + CH)) {
+            if (pend) {  // items of the last batch that start at or above c_prev + MR
+                const bool wr = ((pend >> lane) & 1u) && pd < c + MR;
+                if (wr) {
+                    L.mk[pd & (MR - 1)] = pkey;
+                    if (plit < 0x100u) L.win[pd & (W - 1)] = (uint8_t)plit;
+                }
+                pend &= ~__ballot(wr);
+            }
+            const uint32_t p0 = c + 4 * lane;
+            uint32_t *mkl = L.mk + ((c & (MR - 1)) + 4 * lane);
+            const uint4 m = *(const uint4 *)mkl;
+            const uint32_t lmax = max(max(m.x, m.y), max(m.z, m.w));
+            const uint32_t incl = v4_incl_max(lmax);
+            const uint32_t ex = max(wave_shr1(incl), cin);
+            cin = max(cin, (uint32_t)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(incl, 63)));
+            const uint32_t f0 = max(ex, m.x), f1 = max(f0, m.y), f2 = max(f1, m.z), f3 = max(f2, m.w);
+            uint32_t s0 = p0 - (f0 & 0xffffu), s1 = p0 + 1 - (f1 & 0xffffu);
+            uint32_t s2 = p0 + 2 - (f2 & 0xffffu), s3 = p0 + 3 - (f3 & 0xffffu);
+            PROF_MARK(1);
+            // in-chunk sources of match bytes: s in [c, p)  <=>  s - c < p - c (unsigned)
+            const uint32_t r0 = 4 * lane;
+            bool q0 = s0 - c < r0, q1 = s1 - c < r0 + 1, q2 = s2 - c < r0 + 2, q3 = s3 - c < r0 + 3;
+            if (__ballot(q0 || q1 || q2 || q3)) {
+                // the chunk's marker slots are free once read: they hold each byte's current source
+                uint32_t *spb = L.mk + (c & (MR - 1));
+                *(uint4 *)mkl = make_uint4(s0, s1, s2, s3);
+                do {
+                    const uint32_t t0 = spb[(q0 ? s0 : p0) - c], t1 = spb[(q1 ? s1 : p0 + 1) - c];
+                    const uint32_t t2 = spb[(q2 ? s2 : p0 + 2) - c], t3 = spb[(q3 ? s3 : p0 + 3) - c];
+                    // a byte whose source's source is outside the chunk or a literal is final
+                    q0 = t0 - c < s0 - c, q1 = t1 - c < s1 - c, q2 = t2 - c < s2 - c, q3 = t3 - c < s3 - c;
+                    s0 = t0, s1 = t1, s2 = t2, s3 = t3;
+                    *(uint4 *)mkl = make_uint4(s0, s1, s2, s3);
+#ifdef QLZX_PROFILE
+                    _pacc[7] += 1;
+#endif
+                } while (__ballot(q0 || q1 || q2 || q3));
+            }
+            PROF_MARK(2);
+            const uint32_t lo = c + MR > W ? c + MR - W : 0u;
+            uint32_t v0 = L.win[s0 & (W - 1)], v1 = L.win[s1 & (W - 1)];
+            uint32_t v2 = L.win[s2 & (W - 1)], v3 = L.win[s3 & (W - 1)];
+            if (__ballot(s0 < lo || s1 < lo || s2 < lo || s3 < lo)) {
+                if (s0 < lo) v0 = dst[s0];
+                if (s1 < lo) v1 = dst[s1];
+                if (s2 < lo) v2 = dst[s2];
+                if (s3 < lo) v3 = dst[s3];
+            }
+            const uint32_t w = v0 | (v1 << 8) | (v2 << 16) | (v3 << 24);
+            *(uint32_t *)(L.win + (p0 & (W - 1))) = w;
+            *(uint4 *)mkl = make_uint4(0, 0, 0, 0);  // slots of c + MR .. c + MR + 255
+            PROF_MARK(3);
+            if (c + CH <= dsize) {
+                *(uint32_t *)(dst + p0) = w;
+            } else {
+                for (uint32_t j = 0; j < 4 && p0 + j < dsize; j++) dst[p0 + j] = (uint8_t)(w >> (8 * j));
+            }
+            c += CH;
+            PROF_MARK(4);
+        }
+        return c >= dsize;
+    };
+
+    PROF_DECL
+    for (;;) {
+        if (bt >= nb) { err = true; break; }  // stream ended before dsize (check C5)
+        batch(posmA, tokA, grB, posmB, tokB, grA);
+        PROF_MARK(0);
+        if (err || chunks()) break;
+        if (bt >= nb) { err = true; break; }
+        batch(posmB, tokB, grA, posmA, tokA, grB);
+        PROF_MARK(0);
+        if (err || chunks()) break;
+    }
+    vm_sync();
+    PROF_FLUSH(1);
+    if (lane == 0) {
+        *status_i = err ? QLZX_E_CORRUPT : QLZX_OK;
+        if (dsize_i) *dsize_i = err ? 0u : dsize;
+    }
+}
+
+template <bool CRC>
+__global__ void __launch_bounds__(64) k_dec_chunk4(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
+                                                   uint32_t first, uint32_t count, const BlkInfo *info,
+                                                   const GroupRec *recs, uint32_t gmax, const uint32_t *list,
+                                                   const uint32_t *crc_state, const uint32_t *crc_expect,
+                                                   uint32_t *crc_out) {
+    __shared__ __attribute__((aligned(16))) K2v4Lds L;
+    const uint32_t bx = blockIdx.x;
+    if (bx >= count) return;
+    const uint32_t i = list ? list[bx] : first + bx;
+    if constexpr (CRC) {
+        static_assert(kV4W >= 4096, "the slicing-by-4 CRC tables fill 4 KiB of the window");
+        const uint32_t lane = threadIdx.x;
+        uint32_t *tab = (uint32_t *)L.win;
+        for (uint32_t e = lane * 4; e < 1024; e += 256) *(uint4 *)(tab + e) = *(const uint4 *)(g_crc_slice8 + e);
+        __syncthreads();
+        const uint32_t c = ~wave_crc_rep<4, 1>(tab, g_crc_mul, b.src + b.src_off[i], b.src_len[i],
+                                                crc_state ? crc_state[i] : 0xffffffffu, lane);
+        __syncthreads();
+        if (lane == 0 && crc_out) crc_out[i] = c;
+        if (crc_expect && c != crc_expect[i]) {
+            if (lane == 0) {
+                status[i] = QLZX_E_CRC;
+                if (dsize_out) dsize_out[i] = 0;
+            }
+            return;
+        }
+    }
+    const BlkInfo bi = info[bx];
+    if (bi.kind == kBlkSkip) return;
+    dec_v4_block(L, b.src + b.src_off[i], b.dst + b.dst_off[i], b.src_len[i], bi, recs + (size_t)bx * gmax,
+                 status + i, dsize_out ? dsize_out + i : nullptr, threadIdx.x);
+}
+
+}  // namespace qlzx

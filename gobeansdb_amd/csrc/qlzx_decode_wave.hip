@@ -380,7 +380,20 @@ constexpr uint32_t kWinB = QLZX_K2B_WIN, kMarkRing = QLZX_K2B_MR;
 
 }  // namespace qlzx
 #include "qlzx_decode_solo.hip"
+#include "qlzx_decode_v4.hip"
+#ifndef QLZX_DEC_V4
+#define QLZX_DEC_V4 1
+#endif
 namespace qlzx {
+
+// Set by an atexit handler registered once the runtime is in use (after HIP registered its own
+// teardown; atexit runs in reverse order): per-thread HIP objects destroyed after that (threads
+// exiting during process exit) are left to the runtime's teardown.
+inline std::atomic<bool> g_hip_down{false};
+inline void note_hip_up() {
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit([] { g_hip_down.store(true); }); });
+}
 
 inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uint32_t *dsize,
                               int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
@@ -399,9 +412,17 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     const bool overlap = ws_bytes >= 2 * one && b.n > chunk;
     // per host thread (the batch API is re-entrant like the reference) and per device: the
     // side stream and events are created on the device that owns `s`
-    struct Side {
+    struct Side {  // destroyed with the thread (Go runs cgo calls on many OS threads)
         hipStream_t st = nullptr;
-        hipEvent_t k1[2], k2[2];
+        hipEvent_t k1[2] = {}, k2[2] = {};
+        ~Side() {
+            if (!st || g_hip_down.load()) return;
+            for (int j = 0; j < 2; j++) {
+                if (k1[j]) (void)hipEventDestroy(k1[j]);
+                if (k2[j]) (void)hipEventDestroy(k2[j]);
+            }
+            (void)hipStreamDestroy(st);
+        }
     };
     thread_local Side sides[kMaxDevices];
     hipStream_t side = nullptr;
@@ -418,6 +439,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         if (dev < 0 || dev >= (int)kMaxDevices) return (int)hipErrorInvalidDevice;
         Side &sd = sides[dev];
         if (!sd.st) {
+            note_hip_up();
             (void)hipGetDevice(&cur);
             if (cur != dev) (void)hipSetDevice(dev);
             hipError_t e = hipStreamCreateWithFlags(&sd.st, hipStreamNonBlocking);
@@ -452,11 +474,18 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
         hipStream_t s1 = overlap ? side : s;
         if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
-        hipLaunchKernelGGL(k_dec_parse, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b, dst_cap,
-                           dsize, status, first, cnt, info, recs, gmax, order, max_dsize);
+        hipLaunchKernelGGL(QLZX_DEC_V4 ? k_dec_parse4 : k_dec_parse, dim3((cnt + kParseWG - 1) / kParseWG),
+                           dim3(kParseWG), 0, s1, b, dst_cap, dsize, status, first, cnt, info, recs, gmax, order,
+                           max_dsize);
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
         // one kernel for every block size: the LDS window slides over longer blocks
-        if (crc)
+        if (QLZX_DEC_V4 && crc)
+            hipLaunchKernelGGL(k_dec_chunk4<true>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
+                               recs, gmax, (const uint32_t *)order, crc_state, crc_expect, crc_out);
+        else if (QLZX_DEC_V4)
+            hipLaunchKernelGGL(k_dec_chunk4<false>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
+                               recs, gmax, (const uint32_t *)order, nullptr, nullptr, nullptr);
+        else if (crc)
             hipLaunchKernelGGL((k_dec_bytes<kWinB, kMarkRing, true>), dim3(cnt), dim3(64), 0, s, b, dsize, status,
                                first, cnt, info, recs, gmax, (const uint32_t *)order, crc_state, crc_expect, crc_out);
         else

@@ -125,6 +125,9 @@ def Decompress(source) -> bytes:
     Where Go panics (level not 1/3, an index out of range on a corrupt stream)
     this raises QuicklzError."""
     s = _as_bytes(source)
+    if len(s) == 0 or len(s) < (9 if s[0] & 2 else 3):
+        # SizeDecompressed indexes the size field: Go panics on a short header
+        raise QuicklzError(f"truncated quicklz header ({len(s)} bytes)")
     level = (s[0] >> 2) & 3
     if level not in (1, 3):
         raise QuicklzError("Go version only supports level 1 and 3")
@@ -132,6 +135,10 @@ def Decompress(source) -> bytes:
     dst = ctypes.create_string_buffer(max(n, 1))
     L = _lib.lib()
     if level == 3 and (s[0] & 1):
+        # qlz_decompress reads SizeCompressed(s) bytes (quicklz.c:777-836 trusts the header);
+        # Go indexes source[] and panics once it runs past len(source) (quicklz.go:291-431)
+        if len(s) < SizeCompressed(s):
+            raise QuicklzError(f"truncated quicklz stream: {len(s)} bytes < header csize {SizeCompressed(s)}")
         size = L.qlz_decompress(s, dst, None)
         bad = size != n or L.qlzx_last_status() != _lib.OK
     else:

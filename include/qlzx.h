@@ -67,7 +67,8 @@ enum qlzx_status {
     QLZX_E_HEADER = 6,          /* src_len shorter than the header */
     QLZX_E_EMPTY = 7,           /* compress of an empty value (cquicklz.go:36 panics) */
     QLZX_E_TOO_LARGE = 8,       /* compress size > 0xffffffff-400 (quicklz.c:705) */
-    QLZX_E_MAX_DSIZE = 9        /* dsize > the batch's max_dsize argument (caller contract) */
+    QLZX_E_MAX_DSIZE = 9,       /* dsize > the batch's max_dsize argument (caller contract) */
+    QLZX_E_RUNTIME = 10         /* single call: no result, the GPU runtime failed (qlzx_last_error) */
 };
 
 enum qlzx_return {
@@ -111,7 +112,10 @@ int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_
                           size_t workspace_bytes, void *stream);
 
 /* Compress: replaces CCompress (quicklz/cquicklz.go:23-42) per block.
- *   dst capacity per block must be >= src_len[i] + 400 (cquicklz.go:24)
+ *   dst capacity per block must be >= src_len[i] + 400 (cquicklz.go:24).  The encoder may
+ *                write anywhere in [0, src_len[i] + 400) of a destination (a speculative
+ *                stored copy lands there before the parse decides); only [0, csize[i]) is
+ *                the result, the bytes past it are unspecified.
  *   csize[i]     out: compressed size (0 + status on error)      (required)
  *   status[i]    out: enum qlzx_status                           (nullable)
  *   crc_state / crc_out: as above, over the *compressed* output (the value

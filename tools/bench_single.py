@@ -24,19 +24,49 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 
-def med_us(fn, calls):
+def med_us(fn, calls, pct=None):
     ts = []
     for _ in range(calls):
         t0 = time.perf_counter_ns()
         fn()
         ts.append(time.perf_counter_ns() - t0)
+    if pct is not None:
+        pct["p99"] = round(float(np.percentile(ts, 99)) / 1e3, 2)
     return round(float(np.median(ts)) / 1e3, 2)
+
+
+def aggregate(fn_for_thread, threads, seconds):
+    """Calls/s of `threads` threads each calling its own fn in a loop (ctypes drops the GIL)."""
+    import threading
+    stop = threading.Event()
+    counts = [0] * threads
+    fns = [fn_for_thread(t) for t in range(threads)]
+
+    def worker(t):
+        f = fns[t]
+        c = 0
+        while not stop.is_set():
+            f()
+            c += 1
+        counts[t] = c
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    time.sleep(seconds)
+    stop.set()
+    for th in ths:
+        th.join()
+    return sum(counts) / (time.perf_counter() - t0)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=300)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--threads", type=int, default=16, help="aggregate-throughput callers (0: skip)")
+    ap.add_argument("--seconds", type=float, default=3.0)
     a = ap.parse_args()
     from gobeansdb_amd import _lib
     from oracle import oracle as O
@@ -58,7 +88,10 @@ def main():
         assert L.crc32_write(0xFFFFFFFF, src.ctypes.data, n) == O.crc32_write(0xFFFFFFFF, plain)
         row = {"bytes": n, "ratio": round(len(comp) / n, 3)}
         row["gpu_compress_us"] = med_us(lambda: L.qlz_compress(src.ctypes.data, dst.ctypes.data, n, 0), a.calls)
-        row["gpu_decompress_us"] = med_us(lambda: L.qlz_decompress(csrc.ctypes.data, dst.ctypes.data, 0), a.calls)
+        pct = {}
+        row["gpu_decompress_us"] = med_us(lambda: L.qlz_decompress(csrc.ctypes.data, dst.ctypes.data, 0), a.calls,
+                                          pct)
+        row["gpu_decompress_p99_us"] = pct["p99"]
         row["gpu_crc32_us"] = med_us(lambda: L.crc32_write(0xFFFFFFFF, src.ctypes.data, n), a.calls)
         if ref is not None:
             Q, C = ref
@@ -79,9 +112,24 @@ def main():
                                                                        scratch.ctypes.data), a.calls)
             row["ref_decompress_cgo_us"] = med_us(cgo_decompress, a.calls)
             row["ref_crc32_us"] = med_us(lambda: C.crc32_write(0xFFFFFFFF, src.ctypes.data, n), a.calls)
+        if a.threads:
+            def mk(lib):
+                def for_thread(t):
+                    out = np.zeros(n + 64, np.uint8)
+                    sc = np.zeros(528400, np.uint8)
+                    return lambda: lib.qlz_decompress(csrc.ctypes.data, out.ctypes.data, sc.ctypes.data)
+                return for_thread
+            cps = aggregate(mk(L), a.threads, a.seconds)
+            row["gpu_decompress_threads"] = a.threads
+            row["gpu_decompress_agg_GiBps"] = round(cps * n / 2**30, 3)
+            row["gpu_decompress_agg_calls_per_s"] = round(cps)
+            if ref is not None:
+                cps = aggregate(mk(ref[0]), a.threads, a.seconds)
+                row["ref_decompress_agg_GiBps"] = round(cps * n / 2**30, 3)
         rows.append(row)
         print(json.dumps(row), flush=True)
-    res = {"what": "median per-call latency, one call at a time (ctypes on both sides), text values",
+    res = {"what": "median per-call latency, one call at a time (ctypes on both sides), text values; "
+                   "agg_*: aggregate qlz_decompress rate of --threads concurrent callers",
            "calls_per_point": a.calls, "rows": rows,
            "reference": "oracle/_ref (quicklz.c, crc32.go preamble; gcc -O2)" if ref else None}
     if a.out:
