@@ -101,6 +101,12 @@ def lib() -> ctypes.CDLL:
     L.qlzx_replay_workspace_size.restype = sz
     L.qlzx_replay_index.argtypes = [vp, u64, u64, u32, u64, vp, vp, vp, vp, sz, vp]
     L.qlzx_replay_index.restype = ctypes.c_int
+    L.qlzx_replay_plan_workspace_size.argtypes = [u32]
+    L.qlzx_replay_plan_workspace_size.restype = sz
+    L.qlzx_replay_plan.argtypes = [vp, vp, vp, u32, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
+    L.qlzx_replay_plan.restype = ctypes.c_int
+    L.qlzx_replay_finish.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
+    L.qlzx_replay_finish.restype = ctypes.c_int
     L.qlzx_vhash_batch.argtypes = [vp, vp, vp, u32, vp, vp]
     L.qlzx_vhash_batch.restype = ctypes.c_int
     L.qlzx_last_status.argtypes = []

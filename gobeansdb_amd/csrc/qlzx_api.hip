@@ -16,6 +16,7 @@
 #include "qlzx_crc.hip"
 #include "qlzx_decode_wave.hip"
 #include "qlzx_decode_lane8.hip"
+#include "qlzx_decode_huge.hip"
 #include "qlzx_encode_lane.hip"
 #include "qlzx_encode_wg.hip"
 #include "qlzx_replay.hip"
@@ -105,8 +106,155 @@ int qlz_get_setting(int setting) {  // quicklz.c:31-58 as built by quicklz.h:25-
 size_t qlzx_decompress_workspace_size(uint32_t n, uint32_t max_dsize) {
     // two halves for batches of more than one chunk: K1/K2 of consecutive chunks overlap
     const size_t one = qlzx::decode_wave_ws_bytes(n, max_dsize);
-    return n > qlzx::kChunkBlocks ? 2 * one : one;
+    size_t ws = n > qlzx::kChunkBlocks ? 2 * one : one;
+    if (max_dsize > QLZX_FAST_MAX_DSIZE)  // large values: the pending list and the whole-GPU decoder
+        ws += align_up((size_t)n * sizeof(qlzx::HugeItem) + 256, 256) + qlzx::huge_ws_layout(max_dsize, nullptr, nullptr);
+    return ws;
 }
+
+}  // extern "C"
+
+namespace {
+
+__global__ void k_h_setstatus(int32_t *status, uint32_t *dsize_out, int32_t st, uint32_t ds) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        *status = st;
+        if (dsize_out) *dsize_out = ds;
+    }
+}
+// record CRC verdict of one large block: crc_out, and QLZX_E_CRC (nothing decoded) on a mismatch
+__global__ void k_h_crcverdict(qlzx::HugeCtl *ctl, const uint32_t *crc_expect, uint32_t *crc_out, int32_t *status,
+                               uint32_t *dsize_out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint32_t c = ~ctl->crc;
+    if (crc_out) *crc_out = c;
+    if (crc_expect && c != *crc_expect) {
+        ctl->st = QLZX_E_CRC;
+        *status = QLZX_E_CRC;
+        if (dsize_out) *dsize_out = 0;
+    }
+}
+__global__ void k_h_crcinit(qlzx::HugeCtl *ctl, const uint32_t *crc_state) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) ctl->crc = crc_state ? *crc_state : 0xffffffffu;
+}
+
+// One large block (dsize > QLZX_FAST_MAX_DSIZE) by the whole GPU (qlzx_decode_huge.hip).  The host
+// knows the sizes from the pending list; it synchronises to read the verdict of the parse and
+// the pointer-jumping flags.
+int huge_one(const uint8_t *src, uint32_t csize, uint8_t *dst, uint32_t dsize, bool comp, uint32_t max_dsize,
+             const uint32_t *crc_state, const uint32_t *crc_expect, uint32_t *crc_out, int32_t *status,
+             uint32_t *dsize_out, uint8_t *ws, hipStream_t s) {
+    using namespace qlzx;
+    HugeWs w;
+    huge_ws_layout(max_dsize, ws, &w);
+    const uint32_t nmax = (uint32_t)huge_nmax(max_dsize);
+    const dim3 G(kHugeGrid), B(kHugeWG);
+    HIP_OK(hipMemsetAsync(w.ctl, 0, sizeof(HugeCtl), s));
+    const bool crc = crc_state || crc_expect || crc_out;
+    if (crc) {
+        hipLaunchKernelGGL(k_h_crcseg, dim3(std::min<uint32_t>((csize + kHugeSeg * 4 - 1) / (kHugeSeg * 4), 1024)),
+                           dim3(256), 0, s, src, (uint64_t)csize, w.scrc);
+        hipLaunchKernelGGL(k_h_crcinit, dim3(1), dim3(64), 0, s, w.ctl, crc_state);
+        // the combine reads the initial state from ctl->crc
+        hipLaunchKernelGGL(k_h_crccomb_ctl, dim3(1), dim3(64), 0, s, w.scrc, (uint64_t)csize, w.ctl);
+        hipLaunchKernelGGL(k_h_crcverdict, dim3(1), dim3(64), 0, s, w.ctl, crc_expect, crc_out, status, dsize_out);
+    }
+    const uint32_t hdr = 9;  // header of a value over 64 KiB: always 9 bytes (quicklz.c:771-772)
+    if (!comp) {  // stored (quicklz.c:808-811)
+        if ((uint64_t)csize < (uint64_t)hdr + dsize) {
+            hipLaunchKernelGGL(k_h_setstatus_ok_if, dim3(1), dim3(64), 0, s, w.ctl, status, dsize_out, QLZX_E_CORRUPT, 0u);
+        } else {
+            hipLaunchKernelGGL(k_h_copy_if, G, B, 0, s, w.ctl, src + hdr, dst, (uint64_t)dsize);
+            hipLaunchKernelGGL(k_h_setstatus_ok_if, dim3(1), dim3(64), 0, s, w.ctl, status, dsize_out, QLZX_OK, dsize);
+        }
+        HIP_OK(hipGetLastError());
+        return QLZX_R_OK;
+    }
+    if (csize > nmax) {  // longer than any stream of dsize bytes can be: trailing garbage (C5)
+        hipLaunchKernelGGL(k_h_setstatus_ok_if, dim3(1), dim3(64), 0, s, w.ctl, status, dsize_out, QLZX_E_CORRUPT, 0u);
+        HIP_OK(hipGetLastError());
+        return QLZX_R_OK;
+    }
+    hipLaunchKernelGGL(k_h_codes, G, B, 0, s, src, csize, w.code);
+    hipLaunchKernelGGL(k_h_delta, G, B, 0, s, src, csize, hdr, (const uint32_t *)w.code, w.delta);
+    hipLaunchKernelGGL(k_h_jump1, G, B, 0, s, (const uint8_t *)w.delta, csize, w.J);
+    for (uint32_t k = 2; k <= kHugeLevels; k++)
+        hipLaunchKernelGGL(k_h_jumpk, G, B, 0, s, (const uint16_t *)(w.J + (size_t)(k - 2) * (nmax + 256)), csize,
+                           w.J + (size_t)(k - 1) * (nmax + 256));
+    hipLaunchKernelGGL(k_h_walk, dim3(1), dim3(64), 0, s, src, csize, hdr, dsize, (const uint32_t *)w.code,
+                       (const uint8_t *)w.delta, (const uint16_t *)w.J, nmax, w.seg, w.ctl);
+    hipLaunchKernelGGL(k_h_expand, G, B, 0, s, (const uint8_t *)w.delta, (const HugeSeg *)w.seg,
+                       (const HugeCtl *)w.ctl, w.glist);
+    hipLaunchKernelGGL(k_h_glen, G, B, 0, s, src, csize, (const uint32_t *)w.code, (const uint32_t *)w.glist,
+                       (const HugeCtl *)w.ctl, w.glen);
+    hipLaunchKernelGGL(k_h_scan, dim3(1), dim3(1024), 0, s, w.glen, (const HugeCtl *)w.ctl);
+    hipLaunchKernelGGL(k_h_items, G, B, 0, s, src, csize, hdr, dsize, (const uint32_t *)w.code,
+                       (const uint32_t *)w.glist, (const uint32_t *)w.glen, w.ctl, w.src, w.lit);
+    HIP_OK(hipGetLastError());
+    HugeCtl h;
+    HIP_OK(hipMemcpyAsync(&h, w.ctl, sizeof(HugeCtl), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (h.st == QLZX_E_CRC) return QLZX_R_OK;  // already reported
+    const bool corrupt = h.st != QLZX_OK || h.bad || !h.done || (h.tail_idx != 0xffffffffu && h.max_match > h.tail_idx);
+    if (corrupt) {
+        hipLaunchKernelGGL(k_h_setstatus, dim3(1), dim3(64), 0, s, status, dsize_out, (int32_t)QLZX_E_CORRUPT, 0u);
+        HIP_OK(hipGetLastError());
+        return QLZX_R_OK;
+    }
+    // pointer jumping, four rounds per check of the last round's flag
+    for (uint32_t r = 0;; r += 4) {
+        if (r + 4 > 64) return fail(QLZX_R_HIP, "huge decode: pointer jumping did not converge");
+        for (uint32_t j = 0; j < 4; j++)
+            hipLaunchKernelGGL(k_h_jumpround, G, B, 0, s, w.src, dsize, w.ctl->changed + r + j);
+        uint32_t ch = 0;
+        HIP_OK(hipMemcpyAsync(&ch, w.ctl->changed + r + 3, 4, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        if (!ch) break;
+    }
+    hipLaunchKernelGGL(k_h_gather, G, B, 0, s, (const uint32_t *)w.src, (const uint8_t *)w.lit, dsize, dst);
+    hipLaunchKernelGGL(k_h_setstatus, dim3(1), dim3(64), 0, s, status, dsize_out, (int32_t)QLZX_OK, dsize);
+    HIP_OK(hipGetLastError());
+    return QLZX_R_OK;
+}
+
+// The pending large blocks of a batch (K1 left them kPending): listed on the device, read back
+// once, then decoded one at a time by huge_one.
+int huge_pass(const qlzx_blocks &b, const uint32_t *crc_state, const uint32_t *crc_expect, uint32_t *crc_out,
+              int32_t *status, uint32_t *dsize_out, uint32_t max_dsize, uint8_t *ws, hipStream_t s) {
+    using namespace qlzx;
+    uint32_t *count = (uint32_t *)ws;
+    HugeItem *items = (HugeItem *)(ws + 256);
+    uint8_t *hws = ws + align_up((size_t)b.n * sizeof(HugeItem) + 256, 256);
+    HIP_OK(hipMemsetAsync(count, 0, 4, s));
+    hipLaunchKernelGGL(k_h_pending, dim3(std::min<uint32_t>((b.n + 255) / 256, 4096)), dim3(256), 0, s, b,
+                       (const int32_t *)status, count, items);
+    HIP_OK(hipGetLastError());
+    uint32_t np = 0;
+    HIP_OK(hipMemcpyAsync(&np, count, 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (np == 0) return QLZX_R_OK;
+    std::vector<HugeItem> hl(np);
+    HIP_OK(hipMemcpyAsync(hl.data(), items, np * sizeof(HugeItem), hipMemcpyDeviceToHost, s));
+    std::vector<uint64_t> so(np), dof(np);
+    HIP_OK(hipStreamSynchronize(s));
+    for (uint32_t j = 0; j < np; j++) {
+        HIP_OK(hipMemcpyAsync(&so[j], b.src_off + hl[j].i, 8, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipMemcpyAsync(&dof[j], b.dst_off + hl[j].i, 8, hipMemcpyDeviceToHost, s));
+    }
+    HIP_OK(hipStreamSynchronize(s));
+    for (uint32_t j = 0; j < np; j++) {
+        const uint32_t i = hl[j].i;
+        if (int r = huge_one(b.src + so[j], hl[j].csize, b.dst + dof[j], hl[j].dsize, hl[j].comp != 0, max_dsize,
+                             crc_state ? crc_state + i : nullptr, crc_expect ? crc_expect + i : nullptr,
+                             crc_out ? crc_out + i : nullptr, status + i, dsize_out ? dsize_out + i : nullptr, hws, s))
+            return r;
+    }
+    return QLZX_R_OK;
+}
+
+}  // namespace
+
+extern "C" {
 
 int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_t *dsize,
                           int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
@@ -123,6 +271,12 @@ int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_
         int r = qlzx::launch_decode_wave(*b, dst_cap, dsize, status, crc_state, crc_expect, crc_out,
                                          max_dsize, workspace, workspace_bytes, s);
         if (r) return fail(QLZX_R_HIP, "decode_wave launch", (hipError_t)r);
+    }
+    if (fast && max_dsize > QLZX_FAST_MAX_DSIZE &&
+        workspace_bytes >= qlzx_decompress_workspace_size(b->n, max_dsize)) {
+        // large values: the whole-GPU decoder, one value at a time (synchronises the stream)
+        const size_t wave = qlzx_decompress_workspace_size(b->n, QLZX_FAST_MAX_DSIZE);
+        return huge_pass(*b, crc_state, crc_expect, crc_out, status, dsize, max_dsize, (uint8_t *)workspace + wave, s);
     }
     if (!fast || max_dsize > QLZX_FAST_MAX_DSIZE) {
         const uint32_t min_dsize = fast ? QLZX_FAST_MAX_DSIZE + 1 : 0;
@@ -269,6 +423,36 @@ int qlzx_replay_index(const uint8_t *data, uint64_t size, uint64_t start, uint32
     const int e = qlzx::launch_replay_index(data, size, start, max_key, body_max, rec_off, rec_broken, result,
                                             workspace, (hipStream_t)stream);
     if (e) return fail(QLZX_R_HIP, "qlzx_replay_index", (hipError_t)e);
+    return QLZX_R_OK;
+}
+
+size_t qlzx_replay_plan_workspace_size(uint32_t cap) { return qlzx::replay_plan_ws_bytes(cap); }
+
+int qlzx_replay_plan(const uint8_t *data, const uint64_t *rec_off, const uint32_t *result, uint32_t cap,
+                     int32_t *hdr, uint32_t *comp_idx, uint64_t *comp_off, uint32_t *comp_len, uint32_t *comp_dsize,
+                     uint64_t *comp_dst_off, uint32_t *totals, void *workspace, size_t workspace_bytes, void *stream) {
+    if (!rec_off || !result || !hdr || !comp_idx || !comp_off || !comp_len || !comp_dsize || !comp_dst_off || !totals)
+        return fail(QLZX_R_BAD_ARG, "qlzx_replay_plan: null arg");
+    if (cap && !data) return fail(QLZX_R_BAD_ARG, "qlzx_replay_plan: null data");
+    if (!workspace || workspace_bytes < qlzx::replay_plan_ws_bytes(cap))
+        return fail(QLZX_R_WORKSPACE, "qlzx_replay_plan: workspace too small");
+    const int e = qlzx::launch_replay_plan(data, rec_off, result, cap, hdr, comp_idx, comp_off, comp_len, comp_dsize,
+                                           comp_dst_off, totals, workspace, (hipStream_t)stream);
+    if (e) return fail(QLZX_R_HIP, "qlzx_replay_plan", (hipError_t)e);
+    return QLZX_R_OK;
+}
+
+int qlzx_replay_finish(const uint8_t *data, const uint64_t *rec_off, const uint32_t *result, const uint32_t *totals,
+                       const uint32_t *comp_idx, const int32_t *comp_status, const uint32_t *comp_dsize,
+                       const uint64_t *comp_dst_off, const uint8_t *outbuf, uint32_t cap, int32_t *flag,
+                       int32_t *value_len, uint8_t *in_out, uint64_t *val_off, uint16_t *vhash, void *stream) {
+    if (!rec_off || !result || !totals || !comp_idx || !comp_status || !comp_dsize || !comp_dst_off || !flag ||
+        !value_len || !in_out || !val_off || !vhash)
+        return fail(QLZX_R_BAD_ARG, "qlzx_replay_finish: null arg");
+    const int e = qlzx::launch_replay_finish(data, rec_off, result, totals, comp_idx, comp_status, comp_dsize,
+                                             comp_dst_off, outbuf, cap, flag, value_len, in_out, val_off, vhash,
+                                             (hipStream_t)stream);
+    if (e) return fail(QLZX_R_HIP, "qlzx_replay_finish", (hipError_t)e);
     return QLZX_R_OK;
 }
 

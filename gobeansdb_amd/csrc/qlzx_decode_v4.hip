@@ -21,6 +21,9 @@
 //     token dword, so no prefetched register is copied (and waited for) at a batch boundary.
 //
 // Checks C1-C5 are applied exactly as by the oracle (oracle/qlz_oracle.c:180-231).
+#ifndef QLZX_K1_STRUCT
+#define QLZX_K1_STRUCT 0
+#endif
 namespace qlzx {
 
 // ------------------------------------------------------------------------------- K1 ----
@@ -79,7 +82,47 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
         PROF_MARK(1);
         const bool act = stream && r <= last_round;
         const uint32_t lim = (r + 1) * kRoundBytes - shift;  // stream bytes below lim have landed
-        bool go = act && !done_parse;
+        if (act && !done_parse) {
+#if QLZX_K1_STRUCT
+            // structured steps: a lane leaves the loop when its bytes run out (it resumes next
+            // round) or its stream ends; only active lanes update their state
+            for (;;) {
+#ifdef QLZX_PROFILE
+                _pacc[6] += 1;
+#endif
+                const bool gb = cwr == 1;
+                const uint32_t rem = csize - ip;
+                uint32_t run = __builtin_ctz(cwr);
+                run = run < rem ? run : rem;
+                const uint32_t q = ip + run;
+                const uint32_t rest = cwr >> run;
+                const bool hasm = (rest != 1u) & ((rest & 1u) != 0) & (q < csize);  // gb: rest == 1
+                if (ip + (gb ? 4u : 1u) > csize) { done_parse = true; break; }     // stream exhausted
+                if ((gb | hasm) && q + (gb ? 4u : 1u) > lim) break;                 // wait for the next round
+                const uint32_t w = ring_rd32(ring, q + shift, lane);
+                const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
+                const uint32_t e = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);  // token bytes - 1
+                if (gb) {
+                    if (((w >> 31) == 0) | (g >= gmax)) { st = QLZX_E_CORRUPT; done_parse = true; break; }  // C1
+                    if (g > 0) myrec[g - 1] = GroupRec{rec_ip, cwg, ra, rb};
+                    rec_ip = ip;
+                    cwg = w;
+                    cwr = w;
+                    ra = 0;
+                    rb = 0;
+                    ip += 4;
+                    g++;
+                } else {
+                    if (hasm & (q + e + 1 > csize)) { st = QLZX_E_CORRUPT; done_parse = true; break; }  // C2
+                    const uint32_t kb = hasm ? 1u << (__builtin_clz(cwr) + run) : 0u;
+                    ra |= (e & 1u) ? kb : 0u;
+                    rb |= (e & 2u) ? kb : 0u;
+                    ip = q + (hasm ? e + 1 : 0u);
+                    cwr = rest >> (hasm ? 1 : 0);
+                }
+            }
+#else
+        bool go = true;
         while (__ballot(go)) {
 #ifdef QLZX_PROFILE
             _pacc[5] += 1;
@@ -117,6 +160,8 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
             rb = adv ? nrb : rb;
             done_parse = done_parse | (go & (end | bad));
             go = adv;
+        }
+#endif
         }
         PROF_MARK(3);
         if (done_parse) stream = false;

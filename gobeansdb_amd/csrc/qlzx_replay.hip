@@ -343,6 +343,182 @@ __global__ void __launch_bounds__(64) k_vhash(const uint8_t *src, const uint64_t
     out[i] = (uint16_t)h;
 }
 
+// ---- replay plan / finish (store/item.go:163-176 around the batch decoder, no host parse) ----
+// Per record: its 24-B header, and for the FLAG_COMPRESS ones, in record order, the body's stream
+// offset and length, its decompressed size (the QuickLZ header, quicklz.go:32-44; 0 when the body
+// is shorter than a header, which the decoder reports) and a 256-B-aligned destination offset in
+// one packed output buffer.  totals = {n, ncomp, max_dsize, out_bytes_lo, out_bytes_hi}.
+constexpr uint32_t kFlagCompress = 0x00010000u;
+constexpr uint32_t kBodyMax = 50u << 20;
+struct CompFlag {
+    const uint8_t *data;
+    const uint64_t *off;
+    const uint32_t *result;
+    __device__ uint32_t operator()(uint32_t j) const {
+        return j < result[0] && (((const uint32_t *)(data + off[j]))[2] & kFlagCompress) ? 1u : 0u;
+    }
+};
+__device__ __forceinline__ uint32_t rp_body_dsize(const uint8_t *b, uint32_t len) {
+    if (len < 3) return 0;
+    if (b[0] & 2u) {
+        if (len < 9) return 0;
+        const uint32_t d = b[5] | (b[6] << 8) | (b[7] << 16) | ((uint32_t)b[8] << 24);
+        return d < kBodyMax ? d : kBodyMax;
+    }
+    return b[2];
+}
+struct ScatterComp {
+    const uint8_t *data;
+    const uint64_t *off;
+    uint32_t *comp_idx, *comp_len, *comp_dsize;
+    uint64_t *comp_off;
+    __device__ void operator()(uint32_t j, uint32_t idx, uint32_t v) const {
+        if (!v) return;
+        const uint32_t *h = (const uint32_t *)(data + off[j]);
+        const uint64_t body = off[j] + 24 + h[4];
+        comp_idx[idx] = j;
+        comp_off[idx] = body;
+        comp_len[idx] = h[5];
+        comp_dsize[idx] = rp_body_dsize(data + body, h[5]);
+    }
+};
+__global__ void __launch_bounds__(256) k_rp_headers(const uint8_t *data, const uint64_t *off, const uint32_t *result,
+                                                    int32_t *hdr) {
+    const uint32_t n = result[0];
+    for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+        const uint32_t *h = (const uint32_t *)(data + off[j]);  // records are 256-B aligned
+#pragma unroll
+        for (int k = 0; k < 6; k++) hdr[6 * j + k] = (int32_t)h[k];
+    }
+}
+// destination offsets: exclusive scan of the 256-B-rounded sizes (u64) by one workgroup
+__global__ void __launch_bounds__(1024) k_rp_dstoff(const uint32_t *comp_dsize, const uint32_t *ncomp_p,
+                                                     uint64_t *dst_off, uint32_t *totals, const uint32_t *result) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry;
+    __shared__ uint32_t mx[16];
+    const uint32_t nc = *ncomp_p, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) carry = 0;
+    uint32_t mymax = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nc; base += 1024) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t d = i < nc ? comp_dsize[i] : 0u;
+        mymax = max(mymax, d);
+        const uint64_t v = ((uint64_t)d + 255) & ~(uint64_t)255;
+        uint64_t x = v;
+        for (int k = 1; k < 64; k <<= 1) {
+            const uint64_t y = __shfl_up(x, k, 64);
+            if (lane >= (uint32_t)k) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t acc = 0;
+            for (int j = 0; j < 16; j++) { const uint64_t t = wsum[j]; wsum[j] = acc; acc += t; }
+        }
+        __syncthreads();
+        const uint64_t ex = carry + wsum[w] + x - v;
+        if (i < nc) dst_off[i] = ex;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = ex + v;
+        __syncthreads();
+    }
+    for (int k = 32; k >= 1; k >>= 1) mymax = max(mymax, (uint32_t)__shfl_xor(mymax, k, 64));
+    if (lane == 0) mx[w] = mymax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t m = 0;
+        for (int j = 0; j < 16; j++) m = max(m, mx[j]);
+        totals[0] = result[0];
+        totals[1] = nc;
+        totals[2] = m;
+        totals[3] = (uint32_t)carry;
+        totals[4] = (uint32_t)(carry >> 32);
+    }
+}
+// After the batch decode of the compressed records: flag, value length, where the value lives
+// (decompressed buffer or the raw body: Payload.Decompress errors are swallowed, store/item.go:
+// 163-176) and Getvhash of every record.
+__global__ void __launch_bounds__(256) k_rp_finish_vals(const uint8_t *data, const uint64_t *off, const uint32_t *result,
+                                                       int32_t *flag, int32_t *value_len, uint8_t *in_out,
+                                                       uint64_t *val_off) {
+    for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < result[0]; j += gridDim.x * 256) {
+        const uint32_t *h = (const uint32_t *)(data + off[j]);  // every record: the stored body first
+        flag[j] = (int32_t)h[2];
+        value_len[j] = (int32_t)h[5];
+        in_out[j] = 0;
+        val_off[j] = off[j] + 24 + h[4];
+    }
+}
+__global__ void __launch_bounds__(256) k_rp_finish_comp(const uint32_t *ncomp_p, const uint32_t *comp_idx,
+                                                       const int32_t *cstatus, const uint32_t *cdsize,
+                                                       const uint64_t *cdst_off, int32_t *flag, int32_t *value_len,
+                                                       uint8_t *in_out, uint64_t *val_off) {
+    for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < *ncomp_p; k += gridDim.x * 256) {
+        if (cstatus[k] != QLZX_OK) continue;
+        const uint32_t j = comp_idx[k];
+        flag[j] -= (int32_t)kFlagCompress;  // store/item.go:172-174
+        value_len[j] = (int32_t)cdsize[k];
+        in_out[j] = 1;
+        val_off[j] = cdst_off[k];
+    }
+}
+__global__ void __launch_bounds__(256) k_rp_vhash2(const uint8_t *data, const uint8_t *outbuf, const uint32_t *result,
+                                                  const uint8_t *in_out, const uint64_t *val_off,
+                                                  const int32_t *value_len, uint16_t *vh) {
+    for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < result[0]; j += gridDim.x * 256) {
+        const uint8_t *v = (in_out[j] ? outbuf : data) + val_off[j];
+        const uint32_t l = (uint32_t)value_len[j];
+        uint32_t h = l * 97u;
+        if (l <= 1024) {
+            h += fnv1a_bytes(v, l, 0x811c9dc5u);
+        } else {
+            h += fnv1a_bytes(v, 512, 0x811c9dc5u);
+            h *= 97u;
+            h += fnv1a_bytes(v + l - 512, 512, 0x811c9dc5u);
+        }
+        vh[j] = (uint16_t)h;
+    }
+}
+
+inline size_t replay_plan_ws_bytes(uint32_t cap) { return 256 + (((size_t)cap / kScanTile + 2) * 4 + 255) / 256 * 256; }
+
+inline int launch_replay_plan(const uint8_t *data, const uint64_t *off, const uint32_t *result, uint32_t cap,
+                              int32_t *hdr, uint32_t *comp_idx, uint64_t *comp_off, uint32_t *comp_len,
+                              uint32_t *comp_dsize, uint64_t *comp_dst_off, uint32_t *totals, void *ws,
+                              hipStream_t s) {
+    uint32_t *ncomp = (uint32_t *)ws, *tiles = (uint32_t *)((uint8_t *)ws + 256);
+    const uint32_t ntiles = (cap + kScanTile - 1) / kScanTile;
+    const uint32_t grid = std::min<uint32_t>((cap + 255) / 256, 4096);
+    if (cap == 0) return (int)hipMemsetAsync(totals, 0, 5 * sizeof(uint32_t), s);
+    hipLaunchKernelGGL(k_rp_headers, dim3(grid), dim3(256), 0, s, data, off, result, hdr);
+    CompFlag cf{data, off, result};
+    hipLaunchKernelGGL(k_scan_tiles<CompFlag>, dim3(ntiles), dim3(256), 0, s, cf, cap, tiles);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, tiles, ntiles, ncomp);
+    hipLaunchKernelGGL((k_scan_apply<CompFlag, ScatterComp>), dim3(ntiles), dim3(256), 0, s, cf,
+                       ScatterComp{data, off, comp_idx, comp_len, comp_dsize, comp_off}, cap, tiles);
+    hipLaunchKernelGGL(k_rp_dstoff, dim3(1), dim3(1024), 0, s, (const uint32_t *)comp_dsize, (const uint32_t *)ncomp,
+                       comp_dst_off, totals, result);
+    return (int)hipGetLastError();
+}
+
+inline int launch_replay_finish(const uint8_t *data, const uint64_t *off, const uint32_t *result,
+                                const uint32_t *totals, const uint32_t *comp_idx, const int32_t *cstatus,
+                                const uint32_t *cdsize, const uint64_t *cdst_off, const uint8_t *outbuf,
+                                uint32_t cap, int32_t *flag, int32_t *value_len, uint8_t *in_out, uint64_t *val_off,
+                                uint16_t *vh, hipStream_t s) {
+    if (cap == 0) return 0;
+    const uint32_t grid = std::min<uint32_t>((cap + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_rp_finish_vals, dim3(grid), dim3(256), 0, s, data, off, result, flag, value_len, in_out,
+                       val_off);
+    hipLaunchKernelGGL(k_rp_finish_comp, dim3(grid), dim3(256), 0, s, totals + 1, comp_idx, cstatus, cdsize, cdst_off,
+                       flag, value_len, in_out, val_off);
+    hipLaunchKernelGGL(k_rp_vhash2, dim3(grid), dim3(256), 0, s, data, outbuf, result, (const uint8_t *)in_out,
+                       (const uint64_t *)val_off, (const int32_t *)value_len, vh);
+    return (int)hipGetLastError();
+}
+
 // ---- workspace layout ----
 struct RpWs {
     RpCounters *cnt;

@@ -65,56 +65,73 @@ def index(data: torch.Tensor, start: int = 0, max_key: int = MAX_KEY_LEN, body_m
 
 def replay(data: torch.Tensor, start: int = 0, max_key: int = MAX_KEY_LEN, body_max: int = BODY_MAX,
            workspace: batch.Workspace | None = None, stream=None) -> ReplayResult:
+    """Index, plan, decompress, finish: every per-record step runs on the device
+    (qlzx_replay_index / qlzx_replay_plan / qlzx_decompress_batch / qlzx_replay_finish); the
+    host reads back five numbers once (record and compressed counts, the largest dsize and the
+    output size), which size the output buffer and the decoder launch."""
     L = _lib.lib()
     dev = data.device
     ws = workspace or batch.Workspace(dev)
-    off, broken, end_err, ncand, nvalid = index(data, start, max_key, body_max, ws, stream)
-    n = int(off.numel())
-    # 24-B headers of the records (gathered on device)
-    hidx = off.unsqueeze(1) + torch.arange(HDR, device=dev).unsqueeze(0)
-    hdr = data[hidx.reshape(-1)].reshape(n, HDR).contiguous().view(torch.int32) if n else \
-        torch.zeros((0, 6), dtype=torch.int32, device=dev)
-    flag = hdr[:, 2].clone()
-    ksz = hdr[:, 4].to(torch.int64)
-    vsz = hdr[:, 5].to(torch.int64)
-    body_off = off + HDR + ksz
-    comp = (flag & FLAG_COMPRESS) != 0
-    ci = torch.nonzero(comp).flatten()
-    # values: compressed ones decompressed into a fresh buffer, the others referenced in place
-    value_len = vsz.to(torch.int32).clone()
-    src_base = data
-    val_off = body_off.clone()
-    out = None
-    if ci.numel():
-        csrc = batch.BlockBatch(data, body_off[ci].contiguous(), vsz[ci].to(torch.int32).contiguous())
-        # dsize from each header; Payload.Decompress needs >= 9 B to read it
-        clen = csrc.length.cpu().numpy().view(np.uint32)
-        coff = csrc.off.cpu().numpy().view(np.uint64)
-        host = _headers_dsize(data, coff, clen)
-        out = batch.BlockBatch.empty_for(host, device=dev)
-        dsz, st, _ = batch.decompress(csrc, out, dst_cap=torch.from_numpy(host.view(np.int32)).to(dev),
-                                      max_dsize=int(host.max()) if len(host) else 0, workspace=ws,
-                                      stream=stream)
-        ok = st == 0
-        # successful records: value = decompressed, flag -= FLAG_COMPRESS (store/item.go:172-174)
-        flag[ci[ok]] -= FLAG_COMPRESS
-        value_len[ci[ok]] = dsz[ok]
-    # Getvhash over the final values: gather into one view per source
-    vh = torch.zeros(n, dtype=torch.int32, device=dev)
-    vh16 = torch.zeros(n, dtype=torch.int16, device=dev)
-    plain_i = torch.nonzero(~comp).flatten()
-    if ci.numel():
-        okm = (st == 0)
-        good = ci[okm]
-        bad = ci[~okm]
-        plain_i = torch.cat([plain_i, bad])
-        if good.numel():
-            _vhash(out.data, out.off[okm], value_len[good], vh16, good, stream)
-    if plain_i.numel():
-        _vhash(src_base, val_off[plain_i], value_len[plain_i], vh16, plain_i, stream)
-    vh = vh16.to(torch.int32) & 0xFFFF
-    values = out if out is not None else batch.BlockBatch(data, val_off, value_len)
-    return ReplayResult(off, broken, hdr, flag, value_len, vh, values, end_err, ncand, nvalid)
+    size = int(data.numel())
+    cap = size // 256 + 1
+    st_ = batch._stream(stream)
+    rec_off = torch.empty(cap, dtype=torch.int64, device=dev)
+    rec_broken = torch.empty(cap, dtype=torch.int32, device=dev)
+    result = torch.zeros(4, dtype=torch.int32, device=dev)
+    ws_bytes = L.qlzx_replay_workspace_size(size)
+    w = ws.get(ws_bytes)
+    _lib.check(L.qlzx_replay_index(data.data_ptr() if size else None, size, start, max_key, body_max,
+                                   rec_off.data_ptr(), rec_broken.data_ptr(), result.data_ptr(), w.data_ptr(),
+                                   ws_bytes, st_), "qlzx_replay_index")
+    hdr = torch.empty(cap * 6, dtype=torch.int32, device=dev)
+    comp_idx = torch.empty(cap, dtype=torch.int32, device=dev)
+    comp_off = torch.empty(cap, dtype=torch.int64, device=dev)
+    comp_len = torch.empty(cap, dtype=torch.int32, device=dev)
+    comp_dsize = torch.empty(cap, dtype=torch.int32, device=dev)
+    comp_dst = torch.empty(cap, dtype=torch.int64, device=dev)
+    totals = torch.zeros(5, dtype=torch.int32, device=dev)
+    pws = torch.empty(L.qlzx_replay_plan_workspace_size(cap), dtype=torch.uint8, device=dev)
+    _lib.check(L.qlzx_replay_plan(data.data_ptr() if size else None, rec_off.data_ptr(), result.data_ptr(), cap,
+                                  hdr.data_ptr(), comp_idx.data_ptr(), comp_off.data_ptr(), comp_len.data_ptr(),
+                                  comp_dsize.data_ptr(), comp_dst.data_ptr(), totals.data_ptr(), pws.data_ptr(),
+                                  pws.numel(), st_), "qlzx_replay_plan")
+    # the one read-back: it sizes the output buffer and the decoder launch
+    with torch.cuda.stream(stream) if stream is not None else _nullctx():
+        t = totals.cpu().numpy().view(np.uint32)
+        r = result.cpu().numpy()
+    n, ncomp, maxd = int(t[0]), int(t[1]), int(t[2])
+    out_bytes = int(t[3]) | (int(t[4]) << 32)
+    out = torch.empty(out_bytes + 64, dtype=torch.uint8, device=dev)
+    cst = torch.zeros(max(ncomp, 1), dtype=torch.int32, device=dev)
+    cds = torch.zeros(max(ncomp, 1), dtype=torch.int32, device=dev)
+    values = batch.BlockBatch(out, comp_dst[:ncomp], comp_dsize[:ncomp])
+    if ncomp:
+        csrc = batch.BlockBatch(data, comp_off[:ncomp], comp_len[:ncomp])
+        cds, cst, _ = batch.decompress(csrc, values, dst_cap=comp_dsize[:ncomp], max_dsize=maxd, workspace=ws,
+                                       stream=stream)
+    flag = torch.empty(cap, dtype=torch.int32, device=dev)
+    value_len = torch.empty(cap, dtype=torch.int32, device=dev)
+    in_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    val_off = torch.empty(cap, dtype=torch.int64, device=dev)
+    vh16 = torch.empty(cap, dtype=torch.int16, device=dev)
+    _lib.check(L.qlzx_replay_finish(data.data_ptr() if size else None, rec_off.data_ptr(), result.data_ptr(),
+                                    totals.data_ptr(), comp_idx.data_ptr(), cst.data_ptr(), cds.data_ptr(),
+                                    comp_dst.data_ptr(), out.data_ptr(), cap, flag.data_ptr(), value_len.data_ptr(),
+                                    in_out.data_ptr(), val_off.data_ptr(), vh16.data_ptr(), st_),
+               "qlzx_replay_finish")
+    vh = vh16[:n].to(torch.int32) & 0xFFFF
+    res = ReplayResult(rec_off[:n], rec_broken[:n], hdr[: 6 * n].view(n, 6), flag[:n], value_len[:n], vh, values,
+                       bool(r[1]), int(r[2]), int(r[3]))
+    res.in_out, res.val_off = in_out[:n], val_off[:n]
+    return res
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def _headers_dsize(data: torch.Tensor, off: np.ndarray, length: np.ndarray) -> np.ndarray:

@@ -202,6 +202,28 @@ int qlzx_replay_index(const uint8_t *data, uint64_t size, uint64_t start, uint32
                       uint64_t *rec_off, uint32_t *rec_broken, uint32_t *result, void *workspace,
                       size_t workspace_bytes, void *stream);
 
+/* Around the batch decoder (Payload.Decompress of the FLAG_COMPRESS records, store/item.go:163-176),
+ * without host parsing.  `result` is qlzx_replay_index's (result[0] = n records); `cap` the
+ * capacity of rec_off and of every per-record array below.
+ * qlzx_replay_plan: hdr[6 j..] = the 24-B header of record j (crc, ts, flag, ver, ksz, vsz); the
+ *   compressed records in record order: comp_idx (record), comp_off/comp_len (body in `data`),
+ *   comp_dsize (QuickLZ header dsize, quicklz.go:32-44; 0 if the body is shorter than a header),
+ *   comp_dst_off (256-B-aligned offsets in one packed output buffer);
+ *   totals[5] = {n, ncomp, max dsize, output bytes (lo, hi)} -- the only values a caller needs on
+ *   the host (to size the output buffer and the decoder launch).
+ * qlzx_replay_finish: after qlzx_decompress_batch over the ncomp compressed records (comp_status,
+ *   comp_dsize = its dsize output): per record the flag (FLAG_COMPRESS cleared when the value
+ *   decoded), value_len, where the value lives (in_out 1: outbuf + val_off, 0: data + val_off; a
+ *   failed decode keeps the raw body, as the reference swallows the error) and Getvhash. */
+size_t qlzx_replay_plan_workspace_size(uint32_t cap);
+int qlzx_replay_plan(const uint8_t *data, const uint64_t *rec_off, const uint32_t *result, uint32_t cap,
+                     int32_t *hdr, uint32_t *comp_idx, uint64_t *comp_off, uint32_t *comp_len, uint32_t *comp_dsize,
+                     uint64_t *comp_dst_off, uint32_t *totals, void *workspace, size_t workspace_bytes, void *stream);
+int qlzx_replay_finish(const uint8_t *data, const uint64_t *rec_off, const uint32_t *result, const uint32_t *totals,
+                       const uint32_t *comp_idx, const int32_t *comp_status, const uint32_t *comp_dsize,
+                       const uint64_t *comp_dst_off, const uint8_t *outbuf, uint32_t cap, int32_t *flag,
+                       int32_t *value_len, uint8_t *in_out, uint64_t *val_off, uint16_t *vhash, void *stream);
+
 /* Getvhash (store/item.go:89-100, Fnv1a of utils/hash.go:8-16) of n values. */
 int qlzx_vhash_batch(const uint8_t *src, const uint64_t *off, const uint32_t *len, uint32_t n, uint16_t *out,
                      void *stream);

@@ -104,3 +104,55 @@ def test_large_corrupt_status_matches_oracle(cuda, large):
         assert int(s) == ost
         if ost == 0:
             assert g == od
+
+
+def test_large_values_mixed_with_small_and_record_crc(cuda, large):
+    """Large values (the whole-GPU decoder, qlzx_decode_huge.hip) in one batch with 4-64 KiB
+    values (K1/K2) and a stored large value, with the fused record-CRC verify: a wrong expected
+    CRC on a large value gives QLZX_E_CRC and writes nothing (store/datafile.go:161-168)."""
+    import torch
+    from gobeansdb_amd import batch, _lib
+    big = large["text_1MiB"]
+    stored_plain = np.random.default_rng(3).integers(0, 256, 300_000, dtype=np.uint8).tobytes()
+    stored = O.compress(stored_plain)
+    assert not stored[0] & 1
+    plains = [O.gen_text(31, 0, 16384), big[0], O.gen_text(31, 1, 4096), stored_plain, big[0],
+              O.gen_text(31, 2, 65536)]
+    comps = [O.compress(p) if p is not big[0] else big[1] for p in plains]
+    comps[3] = stored
+    src = batch.BlockBatch.from_bytes(comps)
+    out = batch.BlockBatch.empty_for([len(p) for p in plains])
+    exp = [O.crc32_write(0xFFFFFFFF, c) ^ 0xFFFFFFFF for c in comps]
+    exp[4] ^= 1  # the second copy of the large value: a record whose CRC does not match
+    crc_expect = torch.tensor(np.asarray(exp, np.uint32).view(np.int32), device="cuda")
+    dsz, st, crc = batch.decompress(src, out, max_dsize=max(len(p) for p in plains), want_crc=True,
+                                    crc_state=torch.full((len(plains),), -1, dtype=torch.int32, device="cuda"),
+                                    crc_expect=crc_expect)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy().tolist()
+    assert st == [0, 0, 0, 0, _lib.E_CRC, 0], st
+    dz = dsz.cpu().numpy()
+    assert int(dz[4]) == 0
+    got = out.to_bytes(dz)
+    for k in (0, 1, 2, 3, 5):
+        assert got[k] == plains[k], k
+    c = crc.cpu().numpy().view(np.uint32)
+    assert [int(x) for x in c] == [O.crc32_write(0xFFFFFFFF, x) ^ 0xFFFFFFFF for x in comps]
+
+
+def test_large_all_literal_and_periodic(cuda):
+    """Large values whose groups are all literals (no shortcut needed beyond the sentinel) or all
+    long matches (deep pointer-jumping chains: a period-3 pattern), against the oracle."""
+    import torch
+    from gobeansdb_amd import batch
+    rng = np.random.default_rng(11)
+    lit = (rng.integers(0, 256, 200_000, dtype=np.uint8) & 0x3F).tobytes()  # barely compressible
+    per = np.resize(np.frombuffer(b"xyz", np.uint8), 3 * MIB + 7).tobytes()
+    plains = [lit, per, O.gen_text(5, 0, 65537)]
+    comps = [O.compress(p) for p in plains]
+    src = batch.BlockBatch.from_bytes(comps)
+    out = batch.BlockBatch.empty_for([len(p) for p in plains])
+    dsz, st, _ = batch.decompress(src, out, max_dsize=max(len(p) for p in plains))
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().tolist() == [0, 0, 0]
+    assert out.to_bytes(dsz.cpu().numpy()) == plains
