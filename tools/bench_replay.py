@@ -114,6 +114,41 @@ def build_chunk(mib: int, seed: int, dev):
     return buf, nrec, int(sum(len(v) for v in values[:nrec])), int(sum(sizes[:nrec])), np.asarray(rec_off, np.uint64)
 
 
+def pin_sample(c, res, k: int) -> int:
+    """Full-size parity: every record offset against the chunk's layout, and k sampled records
+    (offset, flag after Payload.Decompress, value bytes, Getvhash) against the oracle's
+    readRecordAt / CDecompressSafe / Getvhash restatements (oracle/replay.py, store/datafile.go:
+    114-170, store/item.go:89-100,163-176) on the host copy of the same chunk."""
+    from oracle import oracle as O
+    from oracle import replay as R
+    n = res.n
+    assert np.array_equal(res.offset.cpu().numpy().view(np.uint64), c["rec_off"][:n].astype(np.uint64)), "offsets"
+    host = c["host"]
+    hb = memoryview(host)
+    rng = np.random.default_rng(20260)
+    picks = sorted(set(rng.integers(0, n, min(k, n)).tolist()))
+    flag = res.flag.cpu().numpy().view(np.uint32)
+    vlen = res.value_len.cpu().numpy()
+    vh = res.vhash.cpu().numpy()
+    in_out = res.in_out.cpu().numpy()
+    voff = res.val_off.cpu().numpy().view(np.uint64)
+    out = res.values.data
+    for j in picks:
+        off = int(c["rec_off"][j])
+        ksz, vsz = struct.unpack_from("<II", host, off + 16)
+        r = R.read_record_at(bytes(hb[off:off + 24 + ksz + vsz]), 0)
+        assert r is not None, j
+        eflag, ebody = r.flag, bytes(r.body)
+        if eflag & R.FLAG_COMPRESS:
+            st, dec = O.decompress(ebody)
+            if st == O.OK:
+                eflag, ebody = eflag - R.FLAG_COMPRESS, dec
+        o, L = int(voff[j]), int(vlen[j])
+        got = out[o:o + L].cpu().numpy().tobytes() if in_out[j] else bytes(hb[o:o + L])
+        assert int(flag[j]) == eflag and got == ebody and int(vh[j]) == R.getvhash(ebody), f"record {j} differs"
+    return len(picks)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--chunk-mib", type=int, default=4000)
@@ -122,6 +157,8 @@ def main():
     p.add_argument("--seed", type=int, default=2026)
     p.add_argument("--cpu-seconds", type=float, default=8.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--pin-records", type=int, default=1024,
+                   help="records per chunk compared with the oracle inside the correctness gate")
     a = p.parse_args()
     rec = run(a, 0, 1, torch.device("cuda", 0))
     print(json.dumps(rec), flush=True)
@@ -157,6 +194,7 @@ def run(a, rank: int, world: int, dev):
         assert int(((res.flag & 0x10000) != 0).sum()) == 0, "a compressed value failed to decode"
         c["compressed"] = int(((res.header[:, 2] & 0x10000) != 0).sum())
         c["out_cap"] = res.values.data.numel()
+        c["pinned_sample"] = pin_sample(c, res, a.pin_records)
         del res
     log("replay verified: all records, all values decoded, both chunks")
     stream = torch.cuda.current_stream(dev)
@@ -239,6 +277,7 @@ def run(a, rank: int, world: int, dev):
                                "(store/datafile.go layout, log-uniform 4-64 KiB values, 70 % text, TryCompress "
                                "policy), replayed as buildHintFromData reads them (store/bucket.go:89-117)",
                    "records_per_chunk": [c["nrec"] for c in chunks],
+                   "oracle_pinned_records": [c["pinned_sample"] for c in chunks],
                    "compressed_values": [c["compressed"] for c in chunks],
                    "chunk_bytes": chunk_b, "parallelism": f"shard{world}"},
         "values_out_gib_per_s": round(tot["out"] / dev_wall / 2**30, 2),
