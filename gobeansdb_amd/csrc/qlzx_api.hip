@@ -433,7 +433,7 @@ int qlzx_replay_plan(const uint8_t *data, const uint64_t *rec_off, const uint32_
                      uint64_t *comp_dst_off, uint32_t *totals, void *workspace, size_t workspace_bytes, void *stream) {
     if (!rec_off || !result || !hdr || !comp_idx || !comp_off || !comp_len || !comp_dsize || !comp_dst_off || !totals)
         return fail(QLZX_R_BAD_ARG, "qlzx_replay_plan: null arg");
-    if (cap && !data) return fail(QLZX_R_BAD_ARG, "qlzx_replay_plan: null data");
+    // data may be null for an empty chunk: nothing is read beyond result[0] = 0 records
     if (!workspace || workspace_bytes < qlzx::replay_plan_ws_bytes(cap))
         return fail(QLZX_R_WORKSPACE, "qlzx_replay_plan: workspace too small");
     const int e = qlzx::launch_replay_plan(data, rec_off, result, cap, hdr, comp_idx, comp_off, comp_len, comp_dsize,

@@ -188,10 +188,119 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
     info[lin] = bi;
 }
 
+// ------------------------------------------------------------- K1 without the LDS ring ----
+// k_dec_parse's step (a literal run and up to two matches, quicklz.c:513-671), reading each step's
+// dword straight from the stream in global memory (L1/L2; a lane's bytes are sequential) instead
+// of an LDS DMA ring: K1 then holds no LDS, so K2 of the previous chunk keeps its occupancy while
+// K1 runs beside it (the 16 KiB ring per K1 wave displaced three K2 waves each).
+__device__ __forceinline__ uint32_t g_rd32(const uint8_t *src, uint32_t q, uint32_t csize) {
+    const uint32_t qa = q + 4 <= csize ? q : csize - 4;  // csize >= 7 for a compressed stream
+    uint64_t a = (uint64_t)(uintptr_t)(src + qa);
+    asm volatile("" : "+v"(a));  // a vector load (any byte address), never a scalar one
+    return *(const uint32_t *)(uintptr_t)a >> (8 * (q - qa));
+}
+__global__ void __launch_bounds__(kParseWG) k_dec_parse_g(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
+                                                      int32_t *status, uint32_t first, uint32_t count, BlkInfo *info,
+                                                      GroupRec *recs, uint32_t gmax, const uint32_t *order,
+                                                      uint32_t max_dsize) {
+    const uint32_t lin = blockIdx.x * kParseWG + threadIdx.x;
+    const bool inrange = lin < count;
+    const uint32_t i = inrange ? (order ? order[lin] : first + lin) : first;
+    int st = QLZX_OK;
+    uint32_t kind = kBlkSkip, csize = 0, dsize = 0, hdr = 0;
+    const uint8_t *src = b.src + b.src_off[i];
+    if (inrange) {
+        st = classify_block(src, b.src_len[i], dst_cap ? dst_cap[i] : 0xffffffffu, max_dsize, kind, csize, dsize, hdr);
+        if (st == QLZX_OK && kind == kBlkCompressed && dsize == 0) {  // oracle/qlz_oracle.c:197,228
+            st = (csize == hdr || csize == hdr + 9) ? QLZX_OK : QLZX_E_CORRUPT;
+            kind = kBlkSkip;
+        }
+    }
+    const bool parsing = inrange && st == QLZX_OK && kind == kBlkCompressed;
+    uint32_t ip = hdr, g = 0, k = 31, cw = 0, m = 0, ra = 0, rb = 0, rec_ip = 0;
+    GroupRec *myrec = recs + (size_t)(inrange ? lin : 0) * gmax;
+    bool done_parse = !parsing, go = parsing;
+    PROF_DECL
+    while (__ballot(go)) {
+#ifdef QLZX_PROFILE
+        _pacc[5] += 1;
+        if (go) _pacc[6] += 1;
+#endif
+        const bool gb = k == 31;
+        const uint32_t kk = k & 31;
+        const uint32_t cwk = cw >> kk;
+        uint32_t run = __builtin_ctz(cwk | (1u << (31 - kk)));  // literals before the next match
+        run = gb ? 0u : (run < csize - ip ? run : csize - ip);
+        const uint32_t ipm = ip + run, km = kk + run;
+        const bool hasm = !gb & (km < 31) & (ipm < csize);
+        const bool end = ip + (gb ? 4u : 1u) > csize;
+        const bool stepping = go & !end & (gb | (run > 0) | hasm);
+        const uint32_t w = g_rd32(src, ipm, csize);
+        const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
+        const uint32_t code = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);
+        const uint32_t ip2 = ipm + code + 1, k2 = km + 1;
+        const uint32_t w2 = w >> (8 * ((code + 1) & 3));
+        const bool mat2 = hasm & (code < 3) & (k2 < 31) & (((cw >> (k2 & 31)) & 1u) != 0) & (ip2 < csize);
+        const uint32_t ty2 = (w2 & 3u) + ((w2 & 127u) == 3u ? 1u : 0u);
+        const uint32_t code2 = __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4);
+        bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) | (hasm & (ipm + code + 1 > csize)) |
+                               (mat2 & (ip2 + code2 + 1 > csize)));
+        if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
+        st = bad ? QLZX_E_CORRUPT : st;
+        const bool adv = stepping & !bad;
+        const bool ag = adv & gb;
+        const uint32_t bm = hasm ? (1u << (km & 31)) : 0u;
+        const uint32_t bm2 = mat2 ? (1u << (k2 & 31)) : 0u;
+        rec_ip = ag ? ip : rec_ip;
+        cw = ag ? w : cw;
+        g += ag ? 1u : 0u;
+        ip += adv ? (gb ? 4u : run + (hasm ? code + 1 : 0u) + (mat2 ? code2 + 1 : 0u)) : 0u;
+        k = adv ? (gb ? 0u : km + (hasm ? 1u : 0u) + (mat2 ? 1u : 0u)) : k;
+        m = adv ? (gb ? 0u : m | bm | bm2) : m;
+        ra = adv ? (gb ? 0u : ra | ((code & 1u) ? bm : 0u) | ((code2 & 1u) ? bm2 : 0u)) : ra;
+        rb = adv ? (gb ? 0u : rb | ((code & 2u) ? bm : 0u) | ((code2 & 2u) ? bm2 : 0u)) : rb;
+        done_parse = done_parse | (go & (end | bad | !stepping));
+        go = adv;
+    }
+    PROF_MARK(3);
+    if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
+    PROF_FLUSH(0);
+    vm_sync();
+    if (!inrange) return;
+    if (st == QLZX_OK && kind == kBlkCompressed && (!done_parse || g == 0)) st = QLZX_E_CORRUPT;
+    BlkInfo bi{0, 0, kind, dsize};
+    if (st != QLZX_OK) {
+        bi.kind = kBlkSkip;
+        status[i] = st;
+        if (dsize_out && st != kPending) dsize_out[i] = 0;
+    } else if (kind == kBlkCompressed) {
+        bi.ngroups = g;
+        bi.nitems = (g - 1) * 31 + (k > 31 ? 31 : k);
+    } else if (kind == kBlkSkip) {  // dsize-0 compressed stream accepted above
+        status[i] = QLZX_OK;
+        if (dsize_out) dsize_out[i] = 0;
+    }
+    info[lin] = bi;
+}
+
 // ------------------------------------------------------------------------------- K2 ----
-constexpr uint32_t kV4W = 4096;   // output window (LDS ring)
-constexpr uint32_t kV4MR = 512;   // marker ring (u32 keys)
-constexpr uint32_t kV4Chunk = 256;
+#ifndef QLZX_K2_BPL
+#define QLZX_K2_BPL 4
+#endif
+#ifndef QLZX_K2_EARLYFAR  // far loads issued before the pointer jumping: measured slower
+#define QLZX_K2_EARLYFAR 0
+#endif
+#ifndef QLZX_K2_WIN
+#define QLZX_K2_WIN 4096
+#endif
+#ifndef QLZX_K2_MR
+#define QLZX_K2_MR 256
+#endif
+constexpr uint32_t kV4W = QLZX_K2_WIN;   // output window (LDS ring)
+constexpr uint32_t kV4MR = QLZX_K2_MR;   // marker ring (u32 keys)
+constexpr uint32_t kV4Bpl = QLZX_K2_BPL;        // output bytes per lane per chunk (4 or 8)
+constexpr uint32_t kV4Chunk = 64 * kV4Bpl;      // 256 or 512 output bytes per chunk
+static_assert(kV4Chunk <= kV4MR, "a chunk's pointer-jumping array lives in its marker slots");
 
 struct K2v4Lds {
     uint8_t win[kV4W];
@@ -229,35 +338,37 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
         if (lane == 0) { *status_i = QLZX_OK; if (dsize_i) *dsize_i = dsize; }
         return;
     }
-    *(uint4 *)(L.mk + lane * 4) = make_uint4(0, 0, 0, 0);
-    *(uint4 *)(L.mk + 256 + lane * 4) = make_uint4(0, 0, 0, 0);
+    for (uint32_t q = lane * 4; q < MR; q += 256) *(uint4 *)(L.mk + q) = make_uint4(0, 0, 0, 0);
 
     const uint32_t nitems = bi.nitems;
     const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
     const uint32_t nb = (nitems + 63) / 64;
     const uint32_t tail_from = dsize > QLZX_TAIL ? dsize - 1 - QLZX_TAIL : 0;  // op >= this: tail (quicklz.c:503)
 
-    auto tok_pos = [&](const GroupRec &gr, const ItemCursor &c, bool v, uint32_t &p) -> uint32_t {
+    // token position of item (c.g, c.k) and its dword address (clamped into the stream; lanes past
+    // the last item read a clamped record and are masked by v where it matters)
+    auto tok_pos = [&](const GroupRec &gr, const ItemCursor &c, uint32_t &p) -> uint32_t {
         const uint32_t low = (1u << c.k) - 1u;
         const uint32_t pos = gr.ip + 4 + c.k + __builtin_popcount(gr.a & low) + 2 * __builtin_popcount(gr.b & low);
-        p = v ? (pos + 4 <= csize ? pos : csize - 4) : 0u;
-        return v ? (pos | (((gr.m >> c.k) & 1u) << 31)) : 0u;
+        p = min(pos, csize - 4);
+        return (pos & 0x7fffffffu) | (((gr.m >> c.k) & 1u) << 31);
     };
+    const uint32_t glast = bi.ngroups - 1;
     // register sets: (posm, tok) of the batch being decoded and of the next; GroupRec of the
     // batch after the decoded one and of the one after that
     ItemCursor ck{lane / 31, lane % 31};
     uint32_t posmA, tokA, posmB = 0, tokB = 0;
     GroupRec grA, grB;
     {
-        const bool v0 = lane < nitems;
-        const GroupRec g0 = rb[v0 ? ck.g : 0u];
+        const GroupRec g0 = rb[min(ck.g, glast)];
         uint32_t tp;
-        posmA = tok_pos(g0, ck, v0, tp);
+        posmA = tok_pos(g0, ck, tp);
         tokA = *(const uint32_t *)(src + tp);
         ck.next();
-        grB = rb[64 + lane < nitems ? ck.g : 0u];
+        grB = rb[min(ck.g, glast)];
         grA = grB;
     }
+    PROF_DECL
     uint32_t D = 0, bt = 0, c = 0, cin = 0;
     bool tail = false, complete = false, err = false;
     uint64_t pend = 0;
@@ -268,18 +379,25 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
     // (posm_n, tok_n) and the GroupRec after it into gr_nn
     auto batch = [&](uint32_t posm, uint32_t tok, const GroupRec &gr_next, uint32_t &posm_n, uint32_t &tok_n,
                      GroupRec &gr_nn) __attribute__((always_inline)) {
+        if (pend) {  // a straddling batch's items not marked by a chunk yet (all start below c + CH)
+            const bool wr = (pend >> lane) & 1u;
+            if (wr) {
+                L.mk[pd & (MR - 1)] = pkey;
+                if (plit < 0x100u) L.win[pd & (W - 1)] = (uint8_t)plit;
+            }
+            pend = 0;
+        }
         const bool v = bt * 64 + lane < nitems;
         {
-            const bool v1 = (bt + 1) * 64 + lane < nitems;
             uint32_t tp;
-            posm_n = tok_pos(gr_next, ck, v1, tp);
+            posm_n = tok_pos(gr_next, ck, tp);
             tok_n = *(const uint32_t *)(src + tp);
             ck.next();
-            gr_nn = rb[(bt + 2) * 64 + lane < nitems ? ck.g : 0u];
+            gr_nn = rb[min(ck.g, glast)];
         }
-        const bool ism = (posm >> 31) != 0;
+        const bool ism = v && (posm >> 31) != 0;
         const uint32_t pos = posm & 0x7fffffffu;
-        const uint32_t t = pos + 4 <= csize ? tok : tok >> (8 * (pos + 4 - csize));
+        const uint32_t t = tok >> (8 * (pos - min(pos, csize - 4)));  // the last tokens: dword clamped
         uint32_t off, mlen, tl;
         decode_tok_bf(t, off, mlen, tl);
         const uint32_t len = ism ? mlen : (v ? 1u : 0u);
@@ -318,6 +436,9 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
         plit = ism ? 0x100u : (t & 0xffu);
         D = __builtin_amdgcn_readfirstlane(D + total);
         bt++;
+#ifdef QLZX_PROFILE
+        _pacc[5] += 1;
+#endif
     };
 
     // chunk phases while every item starting below c + 256 is known; true when the block is done
@@ -331,54 +452,129 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
                 }
                 pend &= ~__ballot(wr);
             }
-            const uint32_t p0 = c + 4 * lane;
-            uint32_t *mkl = L.mk + ((c & (MR - 1)) + 4 * lane);
-            const uint4 m = *(const uint4 *)mkl;
-            const uint32_t lmax = max(max(m.x, m.y), max(m.z, m.w));
+            constexpr uint32_t B = kV4Bpl;
+            const uint32_t r0 = B * lane, p0 = c + r0;
+            uint32_t *mkl = L.mk + ((c & (MR - 1)) + r0);
+            uint32_t m[B], sv[B];
+#pragma unroll
+            for (uint32_t h = 0; h < B; h += 4) {
+                const uint4 q = *(const uint4 *)(mkl + h);
+                m[h] = q.x, m[h + 1] = q.y, m[h + 2] = q.z, m[h + 3] = q.w;
+            }
+            uint32_t lmax = m[0];
+#pragma unroll
+            for (uint32_t j = 1; j < B; j++) lmax = max(lmax, m[j]);
             const uint32_t incl = v4_incl_max(lmax);
-            const uint32_t ex = max(wave_shr1(incl), cin);
+            uint32_t f = max(wave_shr1(incl), cin);
             cin = max(cin, (uint32_t)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(incl, 63)));
-            const uint32_t f0 = max(ex, m.x), f1 = max(f0, m.y), f2 = max(f1, m.z), f3 = max(f2, m.w);
-            uint32_t s0 = p0 - (f0 & 0xffffu), s1 = p0 + 1 - (f1 & 0xffffu);
-            uint32_t s2 = p0 + 2 - (f2 & 0xffffu), s3 = p0 + 3 - (f3 & 0xffffu);
+            bool qa[B], anyq = false;
+#pragma unroll
+            for (uint32_t j = 0; j < B; j++) {
+                f = max(f, m[j]);
+                sv[j] = p0 + j - (f & 0xffffu);
+                // in-chunk sources of match bytes: s in [c, p)  <=>  s - c < p - c (unsigned)
+                qa[j] = sv[j] - c < r0 + j;
+                anyq = anyq || qa[j];
+            }
             PROF_MARK(1);
-            // in-chunk sources of match bytes: s in [c, p)  <=>  s - c < p - c (unsigned)
-            const uint32_t r0 = 4 * lane;
-            bool q0 = s0 - c < r0, q1 = s1 - c < r0 + 1, q2 = s2 - c < r0 + 2, q3 = s3 - c < r0 + 3;
-            if (__ballot(q0 || q1 || q2 || q3)) {
+            const uint32_t lo = c + MR > W ? c + MR - W : 0u;
+#if QLZX_K2_EARLYFAR
+            // bytes whose source is older than the window: their loads go out now and land while
+            // the pointer jumping and the window gather run (sources that jumping changes are in
+            // the chunk, so a byte is far here exactly when its final source is a direct far one)
+            uint32_t fv[B];
+            bool fd[B], anyfd = false;
+#pragma unroll
+            for (uint32_t j = 0; j < B; j++) {
+                fd[j] = sv[j] < lo;
+                anyfd = anyfd || fd[j];
+                fv[j] = 0;
+            }
+            const bool farq = __ballot(anyfd) != 0;
+            if (farq) {
+#pragma unroll
+                for (uint32_t j = 0; j < B; j++)
+                    if (fd[j]) fv[j] = dst[sv[j]];
+            }
+#endif
+            if (__ballot(anyq)) {
                 // the chunk's marker slots are free once read: they hold each byte's current source
                 uint32_t *spb = L.mk + (c & (MR - 1));
-                *(uint4 *)mkl = make_uint4(s0, s1, s2, s3);
+#pragma unroll
+                for (uint32_t h = 0; h < B; h += 4) *(uint4 *)(mkl + h) = make_uint4(sv[h], sv[h + 1], sv[h + 2], sv[h + 3]);
                 do {
-                    const uint32_t t0 = spb[(q0 ? s0 : p0) - c], t1 = spb[(q1 ? s1 : p0 + 1) - c];
-                    const uint32_t t2 = spb[(q2 ? s2 : p0 + 2) - c], t3 = spb[(q3 ? s3 : p0 + 3) - c];
-                    // a byte whose source's source is outside the chunk or a literal is final
-                    q0 = t0 - c < s0 - c, q1 = t1 - c < s1 - c, q2 = t2 - c < s2 - c, q3 = t3 - c < s3 - c;
-                    s0 = t0, s1 = t1, s2 = t2, s3 = t3;
-                    *(uint4 *)mkl = make_uint4(s0, s1, s2, s3);
+                    uint32_t t[B];
+#pragma unroll
+                    for (uint32_t j = 0; j < B; j++) t[j] = spb[(qa[j] ? sv[j] : p0 + j) - c];
+                    anyq = false;
+#pragma unroll
+                    for (uint32_t j = 0; j < B; j++) {
+                        // a byte whose source's source is outside the chunk or a literal is final
+                        qa[j] = t[j] - c < sv[j] - c;
+                        anyq = anyq || qa[j];
+                        sv[j] = t[j];
+                    }
+#pragma unroll
+                    for (uint32_t h = 0; h < B; h += 4)
+                        *(uint4 *)(mkl + h) = make_uint4(sv[h], sv[h + 1], sv[h + 2], sv[h + 3]);
 #ifdef QLZX_PROFILE
                     _pacc[7] += 1;
 #endif
-                } while (__ballot(q0 || q1 || q2 || q3));
+                } while (__ballot(anyq));
             }
             PROF_MARK(2);
-            const uint32_t lo = c + MR > W ? c + MR - W : 0u;
-            uint32_t v0 = L.win[s0 & (W - 1)], v1 = L.win[s1 & (W - 1)];
-            uint32_t v2 = L.win[s2 & (W - 1)], v3 = L.win[s3 & (W - 1)];
-            if (__ballot(s0 < lo || s1 < lo || s2 < lo || s3 < lo)) {
-                if (s0 < lo) v0 = dst[s0];
-                if (s1 < lo) v1 = dst[s1];
-                if (s2 < lo) v2 = dst[s2];
-                if (s3 < lo) v3 = dst[s3];
+            uint32_t vb[B];
+            bool far = false;
+#pragma unroll
+            for (uint32_t j = 0; j < B; j++) {
+                vb[j] = L.win[sv[j] & (W - 1)];
+#if QLZX_K2_EARLYFAR
+                far = far || (sv[j] < lo && !fd[j]);  // reached a far source through the chunk
+#else
+                far = far || sv[j] < lo;
+#endif
             }
-            const uint32_t w = v0 | (v1 << 8) | (v2 << 16) | (v3 << 24);
-            *(uint32_t *)(L.win + (p0 & (W - 1))) = w;
-            *(uint4 *)mkl = make_uint4(0, 0, 0, 0);  // slots of c + MR .. c + MR + 255
+#if QLZX_K2_EARLYFAR
+            if (farq) {
+#pragma unroll
+                for (uint32_t j = 0; j < B; j++) vb[j] = fd[j] ? fv[j] : vb[j];
+            }
+#endif
+#ifdef QLZX_PROFILE
+#if QLZX_K2_EARLYFAR
+            _pacc[6] += (__ballot(far) || farq) ? 1 : 0;  // chunks with a byte older than the window
+#else
+            _pacc[6] += __ballot(far) ? 1 : 0;  // chunks with a byte older than the window
+#endif
+#endif
+#ifndef QLZX_EXP_NOFAR  // (timing experiment: far bytes read from the window, wrong output)
+            if (__ballot(far)) {
+#pragma unroll
+                for (uint32_t j = 0; j < B; j++)
+                    if (sv[j] < lo) vb[j] = dst[sv[j]];
+            }
+#endif
+            uint32_t w[B / 4];
+#pragma unroll
+            for (uint32_t h = 0; h < B / 4; h++)
+                w[h] = vb[4 * h] | (vb[4 * h + 1] << 8) | (vb[4 * h + 2] << 16) | (vb[4 * h + 3] << 24);
+            if constexpr (B == 8) {
+                *(uint2 *)(L.win + (p0 & (W - 1))) = make_uint2(w[0], w[1]);
+            } else {
+                *(uint32_t *)(L.win + (p0 & (W - 1))) = w[0];
+            }
+#pragma unroll
+            for (uint32_t h = 0; h < B; h += 4) *(uint4 *)(mkl + h) = make_uint4(0, 0, 0, 0);  // slots of c + MR ..
             PROF_MARK(3);
             if (c + CH <= dsize) {
-                *(uint32_t *)(dst + p0) = w;
+                if constexpr (B == 8) {
+                    if ((((uintptr_t)dst) & 7u) == 0) *(uint2 *)(dst + p0) = make_uint2(w[0], w[1]);
+                    else *(uint32_t *)(dst + p0) = w[0], *(uint32_t *)(dst + p0 + 4) = w[1];
+                } else {
+                    *(uint32_t *)(dst + p0) = w[0];
+                }
             } else {
-                for (uint32_t j = 0; j < 4 && p0 + j < dsize; j++) dst[p0 + j] = (uint8_t)(w >> (8 * j));
+                for (uint32_t j = 0; j < B && p0 + j < dsize; j++) dst[p0 + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
             }
             c += CH;
             PROF_MARK(4);
@@ -386,7 +582,6 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
         return c >= dsize;
     };
 
-    PROF_DECL
     for (;;) {
         if (bt >= nb) { err = true; break; }  // stream ended before dsize (check C5)
         batch(posmA, tokA, grB, posmB, tokB, grA);
@@ -416,9 +611,9 @@ __global__ void __launch_bounds__(64) k_dec_chunk4(qlzx_blocks b, uint32_t *dsiz
     if (bx >= count) return;
     const uint32_t i = list ? list[bx] : first + bx;
     if constexpr (CRC) {
-        static_assert(kV4W >= 4096, "the slicing-by-4 CRC tables fill 4 KiB of the window");
+        static_assert(sizeof(K2v4Lds) >= 4096, "the slicing-by-4 CRC tables fill 4 KiB of the window");
         const uint32_t lane = threadIdx.x;
-        uint32_t *tab = (uint32_t *)L.win;
+        uint32_t *tab = (uint32_t *)&L;
         for (uint32_t e = lane * 4; e < 1024; e += 256) *(uint4 *)(tab + e) = *(const uint4 *)(g_crc_slice8 + e);
         __syncthreads();
         const uint32_t c = ~wave_crc_rep<4, 1>(tab, g_crc_mul, b.src + b.src_off[i], b.src_len[i],

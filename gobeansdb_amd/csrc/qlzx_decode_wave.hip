@@ -384,6 +384,12 @@ constexpr uint32_t kWinB = QLZX_K2B_WIN, kMarkRing = QLZX_K2B_MR;
 #ifndef QLZX_DEC_V4
 #define QLZX_DEC_V4 1
 #endif
+#ifndef QLZX_K1_GLOBAL  // K1 reading the stream from global memory, no LDS ring (k_dec_parse_g)
+#define QLZX_K1_GLOBAL 0
+#endif
+#ifndef QLZX_K1_V3  // the round-3 K1 (a literal run and up to two matches per step) in front of the v4 K2
+#define QLZX_K1_V3 1
+#endif
 namespace qlzx {
 
 // Set by an atexit handler registered once the runtime is in use (after HIP registered its own
@@ -474,7 +480,8 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
         hipStream_t s1 = overlap ? side : s;
         if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
-        hipLaunchKernelGGL(QLZX_DEC_V4 ? k_dec_parse4 : k_dec_parse, dim3((cnt + kParseWG - 1) / kParseWG),
+        hipLaunchKernelGGL(QLZX_K1_GLOBAL ? k_dec_parse_g : ((QLZX_DEC_V4 && !QLZX_K1_V3) ? k_dec_parse4 : k_dec_parse),
+                           dim3((cnt + kParseWG - 1) / kParseWG),
                            dim3(kParseWG), 0, s1, b, dst_cap, dsize, status, first, cnt, info, recs, gmax, order,
                            max_dsize);
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);

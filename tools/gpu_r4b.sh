@@ -1,16 +1,20 @@
 #!/bin/bash
-# Round 4: v4 decoder pair (k_dec_parse4 + k_dec_chunk4) -- decode parity tests, then A/B timing
-# against the round-3 pair (libqlzx_v3.so = -DQLZX_DEC_V4=0) and kernel traces of both.
+# Round 4: decoder variants -- decode parity tests (default lib), A/B timing (c2, 1 M x 16 KiB)
+# of the round-3 pair (libqlzx_v3.so), the v4 pair (libqlzx.so) and v4 with 8 bytes per lane
+# (libqlzx_b8.so), then kernel traces (whole call and one chunk alone) and v4 phase stamps.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/${OUT:-r04b}; mkdir -p $O
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_decode_bytes.py \
     tests/test_gpu_codec.py tests/test_gpu_sample_parity.py tests/test_gpu_replay.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
-tail -3 $O/tests.log
+tail -1 $O/tests.log
+: > $O/ab.txt
 for rep in 1 2; do
-  for l in gobeansdb_amd/libqlzx_v3.so gobeansdb_amd/libqlzx.so; do
-    QLZX_LIB=$PWD/$l timeout -k 10 180 python -u tools/exp_time.py 1048576 16384 5 2>&1 | grep -v amdgpu.ids | tee -a $O/ab.txt || exit 1
+  for l in v3 v4 b8; do
+    lib=gobeansdb_amd/libqlzx_$l.so; [ $l = v4 ] && lib=gobeansdb_amd/libqlzx.so
+    QLZX_LIB=$PWD/$lib timeout -k 10 180 python -u tools/exp_time.py 1048576 16384 5 2>&1 | grep -v amdgpu.ids | tee -a $O/ab.txt
+    [ ${PIPESTATUS[0]} -gt 100 ] && exit 1
   done
 done
 for l in v3 v4; do
@@ -22,3 +26,4 @@ for l in v3 v4; do
       python3 tools/exp_time.py 131072 16384 3 > $O/alone_$l.txt 2>&1 || { echo alone failed; tail $O/alone_$l.txt; exit 1; }
   python3 tools/kstats.py $(find $O/alone_$l -name "*kernel_trace.csv" | head -1) k_dec k_order | tee $O/alone_medians_$l.txt
 done
+QLZX_LIB=gobeansdb_amd/libqlzx_prof.so timeout -k 10 120 python -u tools/phase_prof.py 131072 16384 2>&1 | grep -v amdgpu.ids | tee $O/phase.txt

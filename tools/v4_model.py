@@ -98,6 +98,12 @@ def k2(src, recs, nitems, dsize, W=4096, MR=512, CH=256):
 
     def batch():
         nonlocal D, bt, tail, complete, pend
+        for (d, key, lit) in pend:  # flush: every pending item starts below c + CH <= c + MR
+            assert d < c + MR
+            mk[d & (MR - 1)] = key
+            if lit is not None:
+                win[d & (W - 1)] = lit
+        pend = []
         items = []
         for lane in range(64):
             I = bt * 64 + lane
@@ -219,7 +225,7 @@ def k2(src, recs, nitems, dsize, W=4096, MR=512, CH=256):
     return 0, bytes(dst)
 
 
-def decode(src):
+def decode(src, ch=256):
     src = bytes(src)
     hdr = 9 if src[0] & 2 else 3
     dsize = O.size_decompressed(src) if hasattr(O, "size_decompressed") else (
@@ -229,7 +235,7 @@ def decode(src):
     st, recs, nitems = k1(src)
     if st:
         return st, None
-    return k2(src, recs, nitems, dsize)
+    return k2(src, recs, nitems, dsize, CH=ch)
 
 
 def main():
@@ -238,11 +244,12 @@ def main():
     cases = [O.gen_text(3, k, n) for k, n in enumerate((1, 5, 13, 64, 255, 256, 257, 1000, 4097, 16384, 30000))]
     cases += [bytes(5000), b"ab" * 3000 + b"c", np.resize(rng.integers(0, 256, 7, dtype=np.uint8), 9000).tobytes()]
     cases += [O.gen_image(4, k, 16384) for k in range(3)]
-    for k, p in enumerate(cases):
-        comp = O.compress(p)
-        st, out = decode(comp)
-        assert st == 0 and out == p, (k, len(p), st)
-    print("v4 model ok on", len(cases), "cases")
+    for ch in (256, 512):
+        for k, p in enumerate(cases):
+            comp = O.compress(p)
+            st, out = decode(comp, ch)
+            assert st == 0 and out == p, (ch, k, len(p), st)
+    print("v4 model ok on", len(cases), "cases, chunks of 256 and 512 B")
 
 
 if __name__ == "__main__":
