@@ -76,8 +76,10 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
         PROF_MARK(0);
 #if QLZX_K1_ROUND == 64
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-#else
+#elif QLZX_K1_ROUND == 32
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#else
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
 #endif
         PROF_MARK(1);
         const bool act = stream && r <= last_round;
@@ -286,6 +288,9 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse_g(qlzx_blocks b, const u
 // ------------------------------------------------------------------------------- K2 ----
 #ifndef QLZX_K2_BPL
 #define QLZX_K2_BPL 4
+#endif
+#ifndef QLZX_K2_ASM_STORE
+#define QLZX_K2_ASM_STORE 0
 #endif
 #ifndef QLZX_K2_EARLYFAR  // far loads issued before the pointer jumping: measured slower
 #define QLZX_K2_EARLYFAR 0
@@ -567,12 +572,21 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
             for (uint32_t h = 0; h < B; h += 4) *(uint4 *)(mkl + h) = make_uint4(0, 0, 0, 0);  // slots of c + MR ..
             PROF_MARK(3);
             if (c + CH <= dsize) {
+#if QLZX_K2_ASM_STORE
+                // stored behind the compiler's back: with no store in its VM_CNT bookkeeping it waits
+                // for a prefetched load with vmcnt(N) instead of draining every store first (vm_sync()
+                // at the end of the block orders them before the status word)
+#pragma unroll
+                for (uint32_t h = 0; h < B / 4; h++)
+                    asm volatile("global_store_dword %0, %1, off" ::"v"(dst + p0 + 4 * h), "v"(w[h]) : "memory");
+#else
                 if constexpr (B == 8) {
                     if ((((uintptr_t)dst) & 7u) == 0) *(uint2 *)(dst + p0) = make_uint2(w[0], w[1]);
                     else *(uint32_t *)(dst + p0) = w[0], *(uint32_t *)(dst + p0 + 4) = w[1];
                 } else {
                     *(uint32_t *)(dst + p0) = w[0];
                 }
+#endif
             } else {
                 for (uint32_t j = 0; j < B && p0 + j < dsize; j++) dst[p0 + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
             }

@@ -50,8 +50,8 @@ constexpr uint32_t kParseWG = 64;
 #define QLZX_CHUNK_BLOCKS 131072
 #endif
 constexpr uint32_t kChunkBlocks = QLZX_CHUNK_BLOCKS;  // >= 256 CUs x 8 waves x 64 lanes: K1 fills the chip
-#ifndef QLZX_K1_ROUND
-#define QLZX_K1_ROUND 64
+#ifndef QLZX_K1_ROUND  // bytes per lane per DMA round: 32 (8 KiB ring per wave) measured best with the v4 K2
+#define QLZX_K1_ROUND 32
 #endif
 constexpr uint32_t kRoundBytes = QLZX_K1_ROUND;  // bytes DMA'd per lane per round (16 B pieces)
 constexpr uint32_t kPieces = kRoundBytes / 16;
@@ -239,8 +239,10 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
 #elif QLZX_K1_ROUND == 32
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#elif QLZX_K1_ROUND == 16
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
 #else
-#error "QLZX_K1_ROUND: 32 or 64"
+#error "QLZX_K1_ROUND: 16, 32 or 64"
 #endif
         PROF_MARK(1);  // 1: waiting for the round's DMA
         const bool act = stream && r <= last_round;
