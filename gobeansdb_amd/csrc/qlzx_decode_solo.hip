@@ -419,21 +419,4 @@ __device__ __forceinline__ void solo_decode(SoloLds &L, const uint8_t *src, uint
     SOLO_STAMP(7);
 }
 
-__global__ void __launch_bounds__(kSoloWG) k_dec_solo(const uint8_t *src, uint32_t len, uint8_t *dst,
-                                                     uint32_t dst_cap, uint32_t max_dsize, GroupRec *recs,
-                                                     int32_t *status, uint32_t *dsize_out) {
-    __shared__ __attribute__((aligned(16))) SoloLds L;
-    solo_decode(L, src, len, dst, dst_cap, max_dsize, recs, status, dsize_out);
-}
-
-// One block (len stream bytes at src, dsize <= QLZX_FAST_MAX_DSIZE, len <= kSoloMaxCsize):
-// recs = kSoloGmax GroupRecs of workspace; status / dsize_out = one device word each.
-inline int launch_decode_solo(const uint8_t *src, uint32_t len, uint8_t *dst, uint32_t dst_cap,
-                              uint32_t max_dsize, GroupRec *recs, int32_t *status, uint32_t *dsize_out,
-                              hipStream_t s) {
-    hipLaunchKernelGGL(k_dec_solo, dim3(1), dim3(kSoloWG), 0, s, src, len, dst, dst_cap, max_dsize, recs,
-                       status, dsize_out);
-    return (int)hipGetLastError();
-}
-
 }  // namespace qlzx

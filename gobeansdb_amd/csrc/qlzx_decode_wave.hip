@@ -382,6 +382,7 @@ constexpr uint32_t kWinB = QLZX_K2B_WIN, kMarkRing = QLZX_K2B_MR;
 
 }  // namespace qlzx
 #include "qlzx_decode_solo.hip"
+#include "qlzx_decode_small.hip"
 #include "qlzx_decode_v4.hip"
 #ifndef QLZX_DEC_V4
 #define QLZX_DEC_V4 1

@@ -69,12 +69,22 @@ __device__ __forceinline__ void svc_publish(SvcDone *done, const SvcReq &r, uint
 
 __global__ void __launch_bounds__(kSoloWG) k_svc_decode(SvcBatch B, const uint8_t *h_arena, uint8_t *d_arena,
                                                         SvcDone *done) {
-    __shared__ __attribute__((aligned(16))) SoloLds L;
+    __shared__ __attribute__((aligned(16))) union {
+        SoloLds solo;
+        SmallLds small;
+    } U;
     __shared__ int32_t st;
     __shared__ uint32_t ds;
     const SvcReq r = B.r[blockIdx.x];
     const uint8_t *hin = h_arena + (size_t)r.slot * kSvcHostSlot;
     uint8_t *hout = (uint8_t *)hin + kSvcIn;
+    // small blocks: stream from the host slot into LDS, result straight into the host slot
+    if (small_decode(U.small, hin, r.len, hout, r.cap, r.cap, &st, &ds)) {
+        __syncthreads();
+        svc_publish(done, r, st == QLZX_OK ? ds : 0u, st, 0);
+        return;
+    }
+    SoloLds &L = U.solo;
     uint8_t *dsrc = d_arena + (size_t)r.slot * kSvcDevSlot, *ddst = dsrc + kSvcIn;
     const uint32_t tid = threadIdx.x;
     svc_copy(dsrc, hin, r.len, tid, kSoloWG);

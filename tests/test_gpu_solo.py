@@ -44,9 +44,11 @@ def _cases():
     rng = np.random.default_rng(11)
     out = []
     for n in (1, 2, 9, 10, 11, 12, 31, 32, 35, 36, 100, 255, 256, 257, 1000, 4095, 4096, 4097, 16383,
-              16384, 16385, 40000, 65535, 65536):
+              16384, 16385, 20000, 32767, 32768, 32769, 40000, 65535, 65536):
         out.append(O.gen_text(0x501, n, n))
-    for n in (64, 4096, 65536):
+    for n in (17000, 17400, 17500):  # stored / compressed around the small path's 17 KiB stream bound
+        out.append(O.gen_image(0x504, n, n))
+    for n in (64, 4096, 30000, 65536):
         out.append(b"a" * n)
         out.append((b"abc" * n)[:n])
         out.append(bytes(rng.integers(0, 4, n, dtype=np.uint8)))
@@ -73,22 +75,40 @@ def test_solo_golden(cuda, golden):
         assert st == 0 and y == x, v["name"]
 
 
-@pytest.mark.parametrize("n", [58000, 65536])
+@pytest.mark.parametrize("n", [15400, 15420, 58000, 65536])
 def test_solo_all_literal_stream(cuda, n):
-    """Literal-only streams: the largest the latency path takes (58000 B -> csize 65493) and one
-    past it (64 KiB -> csize 74005, the batch decoder)."""
+    """Literal-only streams: the largest the small LDS path takes (15400 B -> csize 17397 <= 17408)
+    and one past it (15420 B -> 17421), the largest the latency path takes (58000 B -> csize 65493)
+    and one past it (64 KiB -> csize 74005, the batch decoder)."""
     from gobeansdb_amd import _lib
     L = _lib.lib()
     x = O.gen_image(0x503, n, n)
     c = _all_literal_stream(x)
-    assert (len(c) <= SOLO_MAX_CSIZE) == (n == 58000)
+    assert (len(c) <= SOLO_MAX_CSIZE) == (n != 65536)
+    assert (len(c) <= 17408) == (n == 15400)
     ost, od = O.decompress(c)
     assert ost == 0 and od == x
     st, y = _solo(L, c)
     assert st == 0 and y == x
 
 
-@pytest.mark.parametrize("n", [300, 16384, 65536])
+def test_solo_dsize_zero_streams(cuda):
+    """Compressed streams that declare dsize 0: OK with nothing written iff csize is the header
+    alone or header + 9 (the oracle's C5 rule, oracle/qlz_oracle.c:197,228), else corrupt."""
+    from gobeansdb_amd import _lib
+    L = _lib.lib()
+    cases = []
+    for body in (b"", bytes(9), bytes(5), b"\xff" * 9, (0x80000000).to_bytes(4, "little") + b"abc"):
+        cases.append(bytes([0x4D, 3 + len(body), 0]) + body)
+        cs = 9 + len(body)
+        cases.append(bytes([0x4F]) + cs.to_bytes(4, "little") + bytes(4) + body)
+    for c in cases:
+        ost, od = O.decompress(c)
+        st, y = _solo(L, c)
+        assert st == ost and y == b"", (c.hex(), st, ost)
+
+
+@pytest.mark.parametrize("n", [300, 16384, 30000, 65536])
 def test_solo_corrupt_matches_oracle(cuda, n):
     """Byte flips after the header and truncations (csize field rewritten): status and bytes
     == the oracle's; the batch decoder (K1 + K2b) agrees on the same streams."""

@@ -22,7 +22,8 @@ dev = torch.device("cuda")
 prof = torch.zeros(32, dtype=torch.int64, device=dev)
 assert L.qlzx_profile_set(prof.data_ptr()) == 0
 names = ["codes", "delta+j2", "walk", "recs", "items", "fill", "jumping", "gather"]
-for n in (4096, 16384, 65536):
+names_small = ["stage+info", "J2..J16", "walk+expand", "recs", "items", "fill", "jumping"]
+for n in (4096, 16384, 32768, 65536):
     x = O.gen_text(0x5EED2026, n, n)
     c = O.compress(x)
     out = ctypes.create_string_buffer(n)
@@ -35,7 +36,13 @@ for n in (4096, 16384, 65536):
         L.qlz_decompress(c, out, None)
         ts.append(time.perf_counter_ns() - t0)
     p = prof.cpu().numpy().astype(np.float64)
-    k = max(p[23], 1)
-    ph = {nm: round(p[16 + j] / k) for j, nm in enumerate(names[:7])}
+    if p[31] > 0:  # the small-block LDS path (qlzx_decode_small.hip) took the calls
+        k = p[31]
+        ph = {nm: round(p[24 + j] / k) for j, nm in enumerate(names_small)}
+        ph["(stage)"] = round(p[16] / k)
+        ph["(stage+classify)"] = round(p[17] / k)
+    else:
+        k = max(p[23], 1)
+        ph = {nm: round(p[16 + j] / k) for j, nm in enumerate(names[:7])}
     print(f"{n} B (csize {len(c)}): call median {np.median(ts) / 1e3:.1f} us; kernel cycles {ph}, "
           f"sum {sum(ph.values())}", flush=True)
