@@ -63,6 +63,19 @@ def main():
         torch.distributed.destroy_process_group()
 
 
+def c5_traffic(round_out_bytes: int) -> dict:
+    """PMC HBM bytes of one round (one batch decompress of the resident set): the committed
+    per-output-byte figure (tools/traffic_call.py over a rocprofv3 FETCH_SIZE / WRITE_SIZE run)
+    x this round's decompressed bytes; null when the profile is absent."""
+    path = os.path.join(ROOT, "profiles", "r04_c5_traffic.json")
+    if not os.path.exists(path):
+        return {"traffic": None}
+    tj = json.load(open(path))
+    return {"traffic": round(tj["hbm_bytes_per_call_byte"] * round_out_bytes),
+            "traffic_source": f"profiles/r04_c5_traffic.json: {tj['hbm_bytes_per_call_byte']:.3f} HBM B per output "
+                              f"byte (PMC, one round of {tj['call_bytes'] / 2**30:.1f} GiB out) x bytes per round"}
+
+
 def plan_rounds(total_gib: float, round_gib: float, world: int) -> tuple[int, int]:
     """(rounds, resident bytes per rank): the rank's share of the job in whole rounds of at most
     round_gib, so rounds x resident x world = total_gib at every N (to a block)."""
@@ -175,10 +188,10 @@ def run(args, rank, world, dev):
             "config": {"workload": f"c5: {tot['out'] / 2**30:.0f} GiB of log-uniform 4-64 KiB values "
                                    f"(70 % text / 30 % image-like), {world} rank(s), {rounds} rounds of a "
                                    f"resident {dsum / 2**30:.1f} GiB set per rank",
-                       "blocks_per_round": nblk, "ratio": round(csum / dsum, 3),
+                       "blocks_per_round": nblk, "round_out_bytes": dsum, "ratio": round(csum / dsum, 3),
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4)},
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), **c5_traffic(dsum)},
         }
         return rec
     return None

@@ -165,6 +165,19 @@ def main():
 
 
 HBM_PEAK_GBS = 8000.0
+C4_TRAFFIC = os.path.join(ROOT, "profiles", "r04_c4_traffic.json")
+
+
+def committed_traffic(step_chunk_bytes: float, path: str = C4_TRAFFIC) -> dict:
+    """PMC HBM bytes of one replay step: the committed per-chunk-byte figure of a rocprofv3
+    FETCH_SIZE / WRITE_SIZE run over one replay call (tools/traffic_call.py) x this step's chunk
+    bytes; null when the profile is absent."""
+    if not os.path.exists(path):
+        return {"traffic": None}
+    tj = json.load(open(path))
+    return {"traffic": round(tj["hbm_bytes_per_call_byte"] * step_chunk_bytes),
+            "traffic_source": f"{os.path.relpath(path, ROOT)}: {tj['hbm_bytes_per_call_byte']:.3f} HBM B per chunk "
+                              f"byte (PMC, one replay call of {tj['call_bytes'] / 2**20:.0f} MiB) x chunk bytes per step"}
 
 
 def run(a, rank: int, world: int, dev):
@@ -282,7 +295,7 @@ def run(a, rank: int, world: int, dev):
                    "chunk_bytes": chunk_b, "parallelism": f"shard{world}"},
         "values_out_gib_per_s": round(tot["out"] / dev_wall / 2**30, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), **committed_traffic(steps_chunk / a.steps),
                      "what": "per step: every chunk byte read once (scan + CRC) + every value byte written",
                      "kernel_ms": round(dev_ev * 1e3 / a.steps, 3)},
         "end_to_end_pipelined": {"files": a.files, "total_gib": round(tot["e2e"] / 2**30, 2),
