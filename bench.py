@@ -322,7 +322,8 @@ def main():
         import bench_replay as c4mod
         a4 = argparse.Namespace(chunk_mib=256 if args.legs_small else args.c4_chunk_mib,
                                 files=4 if args.legs_small else args.c4_files, steps=4, seed=2026,
-                                cpu_seconds=max(2.0, args.cpu_seconds / 2), no_cpu=args.no_cpu)
+                                cpu_seconds=max(2.0, args.cpu_seconds / 2), no_cpu=args.no_cpu,
+                                pin_records=64 if args.legs_small else 1024)
         replay_rec = c4mod.run(a4, rank, world, dev)
         torch.cuda.synchronize()
         torch.cuda.empty_cache()

@@ -292,6 +292,9 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse_g(qlzx_blocks b, const u
 #ifndef QLZX_K2_ASM_STORE
 #define QLZX_K2_ASM_STORE 0
 #endif
+#ifndef QLZX_K2_PRIO  // wave priority of K2 (s_setprio) over the overlapped K1
+#define QLZX_K2_PRIO 0
+#endif
 #ifndef QLZX_K2_EARLYFAR  // far loads issued before the pointer jumping: measured slower
 #define QLZX_K2_EARLYFAR 0
 #endif
@@ -621,6 +624,10 @@ __global__ void __launch_bounds__(64) k_dec_chunk4(qlzx_blocks b, uint32_t *dsiz
                                                    const uint32_t *crc_state, const uint32_t *crc_expect,
                                                    uint32_t *crc_out) {
     __shared__ __attribute__((aligned(16))) K2v4Lds L;
+#if QLZX_K2_PRIO
+    // K2 waves first when they share a SIMD with the next chunk's K1 (which has slack)
+    __builtin_amdgcn_s_setprio(QLZX_K2_PRIO);
+#endif
     const uint32_t bx = blockIdx.x;
     if (bx >= count) return;
     const uint32_t i = list ? list[bx] : first + bx;
