@@ -158,7 +158,7 @@ __device__ uint32_t wave_crc(const uint32_t *lds, const uint8_t *p, uint64_t len
 // S4: tab holds the slicing-by-4 tables instead (g_crc_slice8[0..1023], 4 KiB, no copies): four
 // independent lookups per dword instead of a chain of four, one VALU less per byte, more conflicts.
 template <uint32_t R, bool S4 = false>
-__device__ uint32_t wave_crc_rep(const uint32_t *tab, const uint32_t *mul, const uint8_t *p, uint64_t len,
+__device__ __forceinline__ uint32_t wave_crc_rep(const uint32_t *tab, const uint32_t *mul, const uint8_t *p, uint64_t len,
                                  uint32_t init, uint32_t lane) {
     const uint32_t *tr = S4 ? tab : tab + (lane & (R - 1));
     if (len < 4) {

@@ -292,6 +292,9 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse_g(qlzx_blocks b, const u
 #ifndef QLZX_K2_ASM_STORE
 #define QLZX_K2_ASM_STORE 0
 #endif
+#ifndef QLZX_K2_FARSPLIT
+#define QLZX_K2_FARSPLIT 0
+#endif
 #ifndef QLZX_K2_PRIO  // wave priority of K2 (s_setprio) over the overlapped K1
 #define QLZX_K2_PRIO 0
 #endif
@@ -555,6 +558,25 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
             _pacc[6] += __ballot(far) ? 1 : 0;  // chunks with a byte older than the window
 #endif
 #endif
+            uint32_t w[B / 4];
+#if QLZX_K2_FARSPLIT
+            // the far loads' wait stays inside their branch: a chunk without far bytes does not
+            // wait for the previous chunk's store and the prefetched loads at a merged vmcnt(0)
+            if (__ballot(far)) {
+#pragma unroll
+                for (uint32_t j = 0; j < B; j++)
+                    if (sv[j] < lo) vb[j] = dst[sv[j]];
+#pragma unroll
+                for (uint32_t h = 0; h < B / 4; h++) {
+                    w[h] = vb[4 * h] | (vb[4 * h + 1] << 8) | (vb[4 * h + 2] << 16) | (vb[4 * h + 3] << 24);
+                    asm volatile("" : "+v"(w[h]));
+                }
+            } else {
+#pragma unroll
+                for (uint32_t h = 0; h < B / 4; h++)
+                    w[h] = vb[4 * h] | (vb[4 * h + 1] << 8) | (vb[4 * h + 2] << 16) | (vb[4 * h + 3] << 24);
+            }
+#else
 #ifndef QLZX_EXP_NOFAR  // (timing experiment: far bytes read from the window, wrong output)
             if (__ballot(far)) {
 #pragma unroll
@@ -562,10 +584,10 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
                     if (sv[j] < lo) vb[j] = dst[sv[j]];
             }
 #endif
-            uint32_t w[B / 4];
 #pragma unroll
             for (uint32_t h = 0; h < B / 4; h++)
                 w[h] = vb[4 * h] | (vb[4 * h + 1] << 8) | (vb[4 * h + 2] << 16) | (vb[4 * h + 3] << 24);
+#endif
             if constexpr (B == 8) {
                 *(uint2 *)(L.win + (p0 & (W - 1))) = make_uint2(w[0], w[1]);
             } else {

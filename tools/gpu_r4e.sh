@@ -24,6 +24,10 @@ sq() {  # $1 tag, $2 lib
     python3 tools/pmc_sum.py $O/sq_$1/p$PASS 2>&1 | tee -a $O/sq_counters_$1.txt
   done
 }
+for l in $CRCV; do  # c2 with the fused record CRC (K2<true>)
+  lib=gobeansdb_amd/libqlzx_$l.so; [ $l = v4 ] && lib=gobeansdb_amd/libqlzx.so
+  QLZX_CRC=1 QLZX_LIB=$PWD/$lib timeout -k 10 180 python -u tools/exp_time.py 1048576 16384 5 2>&1 | grep -v amdgpu.ids | sed "s/^/crc /" | tee -a $O/ab.txt
+done
 [ -n "$NOSQ" ] && exit 0
 sq v3 gobeansdb_amd/libqlzx_v3.so || exit 1
 sq v4 gobeansdb_amd/libqlzx.so || exit 1
