@@ -19,6 +19,7 @@
 #include "qlzx_decode_huge.hip"
 #include "qlzx_encode_lane.hip"
 #include "qlzx_encode_wg.hip"
+#include "qlzx_encode_huge.hip"
 #include "qlzx_replay.hip"
 #include "qlzx_record.hip"
 #include "qlzx_level1.hip"
@@ -252,6 +253,128 @@ int huge_pass(const qlzx_blocks &b, const uint32_t *crc_state, const uint32_t *c
     return QLZX_R_OK;
 }
 
+__global__ void k_he_fail(int32_t *status, uint32_t *csize, int32_t st) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (status) *status = st;
+    *csize = 0;
+}
+__global__ void k_he_crcfin(const uint32_t *scrc, uint64_t len, const uint32_t *crc_state, uint32_t *crc_out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint32_t nseg = (uint32_t)((len + qlzx::kHugeSeg - 1) / qlzx::kHugeSeg);
+    uint32_t acc = *crc_state;
+    for (uint32_t k = 0; k < nseg; k++)
+        acc = qlzx::crc_shift(acc, min((uint64_t)qlzx::kHugeSeg, len - (uint64_t)k * qlzx::kHugeSeg)) ^ scrc[k];
+    *crc_out = ~acc;  // as the lane encoder: ~crc over the output from crc_state
+}
+
+// One value of n > 64 KiB bytes by the whole GPU (qlzx_encode_huge.hip).  The host synchronises
+// twice: for the parse's item count, and for the bail-out verdict and the output size.
+int huge_encode_one(const uint8_t *src, uint32_t n, uint8_t *dst, uint32_t flags, const uint32_t *crc_state,
+                    uint32_t *crc_out, uint32_t *csize_out, int32_t *status, uint32_t nmax, uint8_t *ws,
+                    hipStream_t s) {
+    using namespace qlzx;
+    HeWs w;
+    he_ws_layout(nmax, ws, &w);
+    const uint32_t P = he_positions(n), L = he_levels(P);
+    const dim3 G(kHeGrid), B(kHeWG);
+    HIP_OK(hipMemsetAsync(w.ctl, 0, sizeof(HeCtl), s));
+    hipLaunchKernelGGL(k_he_keys, G, B, 0, s, src, P, w.key, w.pos);
+    size_t tb = w.tmp_bytes;
+    if (rocprim::radix_sort_pairs(w.tmp, tb, (const uint16_t *)w.key, w.key_s, (const uint32_t *)w.pos, w.pos_s,
+                                  (size_t)P, 0, 12, s) != hipSuccess)
+        return fail(QLZX_R_HIP, "huge encode: radix sort");
+    hipLaunchKernelGGL(k_he_base, G, B, 0, s, (const uint16_t *)w.key_s, P, w.base);
+    hipLaunchKernelGGL(k_he_match, G, B, 0, s, src, n, P, (const uint16_t *)w.key_s, (const uint32_t *)w.pos_s,
+                       (const uint32_t *)w.base, w.MO);
+    hipLaunchKernelGGL(k_he_jump0, G, B, 0, s, (const uint32_t *)w.MO, P, w.J);
+    for (uint32_t k = 1; k < L; k++)
+        hipLaunchKernelGGL(k_he_jumpk, G, B, 0, s, (const uint32_t *)(w.J + (size_t)(k - 1) * (P + 1)), P,
+                           w.J + (size_t)k * (P + 1));
+    hipLaunchKernelGGL(k_he_walk, dim3(1), dim3(64), 0, s, (const uint32_t *)w.J, P, L, (const uint32_t *)w.MO,
+                       w.ITEM, w.ctl);
+    for (uint32_t k = L - 1; k >= 1; k--)
+        hipLaunchKernelGGL(k_he_expand, G, B, 0, s, (const uint32_t *)(w.J + (size_t)(k - 1) * (P + 1)),
+                           (const HeCtl *)w.ctl, k, w.ITEM);
+    HIP_OK(hipGetLastError());
+    HeCtl h;
+    HIP_OK(hipMemcpyAsync(&h, w.ctl, sizeof(HeCtl), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (h.tail0 > n || h.m > P) return fail(QLZX_R_HIP, "huge encode: parse out of range");
+    const uint32_t ntot = h.m + (n - h.tail0);
+    hipLaunchKernelGGL(k_he_sizes, G, B, 0, s, (const uint32_t *)w.ITEM, (const uint32_t *)w.MO,
+                       (const HeCtl *)w.ctl, ntot, w.sizes);
+    tb = w.tmp_bytes;
+    if (rocprim::exclusive_scan(w.tmp, tb, (const uint32_t *)w.sizes, w.S, 0u, (size_t)ntot + 1,
+                                rocprim::plus<uint32_t>(), s) != hipSuccess)
+        return fail(QLZX_R_HIP, "huge encode: scan");
+    const uint32_t bias = (flags & QLZX_F_GO_COMPAT) ? 9u : 0u;  // Go counts the header (quicklz.go:119)
+    hipLaunchKernelGGL(k_he_bail, G, B, 0, s, (const uint32_t *)w.ITEM, (const uint32_t *)w.S, n, bias, w.ctl);
+    uint32_t tot = 0;
+    HIP_OK(hipMemcpyAsync(&tot, w.S + ntot, 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(&h, w.ctl, sizeof(HeCtl), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    const uint32_t hdr = 9;  // n > 64 KiB >= 216 (quicklz.c:708-711)
+    uint32_t cs;
+    if (!h.bail) {
+        const uint32_t core = 4 * ((ntot + 30) / 31) + tot;
+        cs = hdr + core;
+        hipLaunchKernelGGL(k_he_write, G, B, 0, s, src, (const uint32_t *)w.ITEM, (const uint32_t *)w.MO,
+                           (const uint32_t *)w.S, (const HeCtl *)w.ctl, ntot, dst + hdr);
+    } else {  // stored (quicklz.c:722-727)
+        cs = n + hdr;
+        hipLaunchKernelGGL(k_he_copy, G, B, 0, s, src, dst + hdr, (uint64_t)n);
+    }
+    hipLaunchKernelGGL(k_he_header, dim3(1), dim3(64), 0, s, dst, !h.bail, cs, n, csize_out, status);
+    if (crc_state && crc_out) {
+        hipLaunchKernelGGL(k_h_crcseg, dim3(std::min<uint32_t>((cs + kHugeSeg * 4 - 1) / (kHugeSeg * 4), 1024)),
+                           dim3(256), 0, s, (const uint8_t *)dst, (uint64_t)cs, w.scrc);
+        hipLaunchKernelGGL(k_he_crcfin, dim3(1), dim3(64), 0, s, (const uint32_t *)w.scrc, (uint64_t)cs, crc_state,
+                           crc_out);
+    }
+    HIP_OK(hipGetLastError());
+    return QLZX_R_OK;
+}
+
+// The values over 64 KiB of a compress batch: listed on the device, read back once, then
+// compressed one at a time by huge_encode_one.
+int huge_encode_pass(const qlzx_blocks &b, uint32_t *csize, int32_t *status, const uint32_t *crc_state,
+                     uint32_t *crc_out, uint32_t flags, uint32_t max_len, uint8_t *ws, hipStream_t s) {
+    using namespace qlzx;
+    uint32_t *count = (uint32_t *)ws;
+    HeItem *items = (HeItem *)(ws + 256);
+    uint8_t *hws = ws + align_up((size_t)std::max<uint32_t>(b.n, 1) * sizeof(HeItem) + 256, 256);
+    HIP_OK(hipMemsetAsync(count, 0, 4, s));
+    hipLaunchKernelGGL(k_he_pending, dim3(std::min<uint32_t>((b.n + 255) / 256, 4096)), dim3(256), 0, s, b,
+                       (uint32_t)QLZX_WG_MAX_LEN + 1, count, items);
+    HIP_OK(hipGetLastError());
+    uint32_t np = 0;
+    HIP_OK(hipMemcpyAsync(&np, count, 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (np == 0) return QLZX_R_OK;
+    std::vector<HeItem> hl(np);
+    HIP_OK(hipMemcpyAsync(hl.data(), items, np * sizeof(HeItem), hipMemcpyDeviceToHost, s));
+    std::vector<uint64_t> so(np), dof(np);
+    HIP_OK(hipStreamSynchronize(s));
+    for (uint32_t j = 0; j < np; j++) {
+        HIP_OK(hipMemcpyAsync(&so[j], b.src_off + hl[j].i, 8, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipMemcpyAsync(&dof[j], b.dst_off + hl[j].i, 8, hipMemcpyDeviceToHost, s));
+    }
+    HIP_OK(hipStreamSynchronize(s));
+    for (uint32_t j = 0; j < np; j++) {
+        const uint32_t i = hl[j].i;
+        if (hl[j].n > max_len || (uint64_t)hl[j].n > 0xffffffffull - 400) {  // as the lane encoder reports it
+            hipLaunchKernelGGL(k_he_fail, dim3(1), dim3(64), 0, s, status ? status + i : nullptr, csize + i,
+                               (int32_t)QLZX_E_TOO_LARGE);
+            continue;
+        }
+        if (int r = huge_encode_one(b.src + so[j], hl[j].n, b.dst + dof[j], flags, crc_state ? crc_state + i : nullptr,
+                                    crc_out ? crc_out + i : nullptr, csize + i, status ? status + i : nullptr, max_len,
+                                    hws, s))
+            return r;
+    }
+    return QLZX_R_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -290,9 +413,13 @@ int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_
 size_t qlzx_compress_workspace_size(uint32_t n, uint32_t max_len) {
     // at least one lane slab: QLZX_F_GO_COMPAT batches (flags are not known here) take the lane path
     size_t ws = qlzx::kLaneSlab;
-    if (max_len > QLZX_WG_MAX_LEN || !qlzx::encode_wg_enabled())
+    if (!qlzx::encode_wg_enabled())
         ws = (size_t)std::min<uint32_t>(std::max<uint32_t>(n, 1), kMaxLaneSlabs) * qlzx::kLaneSlab;
-    return std::max(ws, qlzx::encode_wg_ws_bytes(n, max_len));
+    ws = std::max(ws, qlzx::encode_wg_ws_bytes(n, max_len));
+    if (max_len > QLZX_WG_MAX_LEN)  // values over 64 KiB: the pending list and the whole-GPU encoder
+        ws += align_up((size_t)std::max<uint32_t>(n, 1) * sizeof(qlzx::HeItem) + 256, 256) +
+              qlzx::he_ws_layout(max_len, nullptr, nullptr);
+    return ws;
 }
 
 int qlzx_compress_batch(const qlzx_blocks *b, uint32_t *csize, int32_t *status,
@@ -306,19 +433,22 @@ int qlzx_compress_batch(const qlzx_blocks *b, uint32_t *csize, int32_t *status,
         return fail(QLZX_R_WORKSPACE, "qlzx_compress_batch: workspace too small");
     hipStream_t s = (hipStream_t)stream;
     const bool wg = qlzx::encode_wg_enabled() && !(flags & QLZX_F_GO_COMPAT);
+    const bool huge = max_len > QLZX_WG_MAX_LEN;  // values over 64 KiB: qlzx_encode_huge.hip
     if (wg) {
         int r = qlzx::launch_encode_wg(*b, csize, status, crc_state, crc_out, max_len, flags, workspace, s);
         if (r) return fail(QLZX_R_HIP, "encode_wg launch", (hipError_t)r);
     }
-    if (!wg || max_len > QLZX_WG_MAX_LEN) {
+    if (!wg) {  // the lane encoder: Go-compat batches (and a disabled workgroup encoder) up to 64 KiB
         const uint32_t nl = (uint32_t)std::min<size_t>(
             std::min<uint32_t>(b->n, kMaxLaneSlabs), workspace_bytes / qlzx::kLaneSlab);
         if (nl == 0) return fail(QLZX_R_WORKSPACE, "qlzx_compress_batch: no lane slab");
-        const uint32_t min_len = wg ? QLZX_WG_MAX_LEN + 1 : 0;
         hipLaunchKernelGGL(qlzx::k_encode_lane, dim3((nl + 63) / 64), dim3(64), 0, s, *b, csize, status,
-                           crc_state, crc_out, (uint8_t *)workspace, nl, min_len, flags);
+                           crc_state, crc_out, (uint8_t *)workspace, nl, 0u, huge ? (uint32_t)QLZX_WG_MAX_LEN : 0u,
+                           flags);
         HIP_OK(hipGetLastError());
     }
+    if (huge)  // after the kernels above in stream order: the whole workspace is free again
+        return huge_encode_pass(*b, csize, status, crc_state, crc_out, flags, max_len, (uint8_t *)workspace, s);
     return QLZX_R_OK;
 }
 

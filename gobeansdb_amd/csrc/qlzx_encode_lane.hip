@@ -132,11 +132,11 @@ __device__ uint32_t compress_block_lane(const uint8_t *src, uint32_t n, uint8_t 
 }
 
 // Grid-stride over blocks; lane t owns slab t of the workspace.  Blocks with
-// src_len < min_len are skipped (owned by the fast path when it runs).
+// src_len < min_len (the fast path) or > max_len (the whole-GPU path) are skipped (0: no bound).
 __global__ void __launch_bounds__(64) k_encode_lane(qlzx_blocks b, uint32_t *csize, int32_t *status,
                                                     const uint32_t *crc_state, uint32_t *crc_out,
                                                     uint8_t *ws, uint32_t nlanes, uint32_t min_len,
-                                                    uint32_t flags) {
+                                                    uint32_t max_len, uint32_t flags) {
     __shared__ uint32_t tab[256];
     load_crc_table(tab);
     __syncthreads();
@@ -148,6 +148,7 @@ __global__ void __launch_bounds__(64) k_encode_lane(qlzx_blocks b, uint32_t *csi
     for (uint32_t i = t; i < b.n; i += nlanes) {
         const uint32_t n = b.src_len[i];
         if (min_len && n < min_len) continue;  // the workgroup kernel owns it (including n == 0)
+        if (max_len && n > max_len) continue;  // the whole-GPU encoder owns it (qlzx_encode_huge.hip)
         int st = QLZX_OK;
         uint8_t *dst = b.dst + b.dst_off[i];
         const uint32_t r = compress_block_lane(b.src + b.src_off[i], n, dst, slots, count, flags, st);

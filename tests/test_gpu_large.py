@@ -1,6 +1,6 @@
 """GPU parity for values far above 64 KiB, up to BodyMax (50 MiB, config/mc_config.go:8):
-the general kernels k_encode_lane (values > 64 KiB) and k_dec_lane8 (dsize > 64 KiB) against
-the oracle, including long literal runs (the byte-serial loop of k_dec_lane8) and corrupted
+the whole-GPU encoder (qlzx_encode_huge.hip) and decoder (qlzx_decode_huge.hip, k_dec_lane8 without
+a workspace) against the oracle, including long literal runs (the byte-serial loop of k_dec_lane8) and corrupted
 streams of such values.  Offsets >= 131071 (quicklz.c:361 falls back to literals) occur at
 these sizes."""
 import numpy as np
@@ -59,8 +59,8 @@ def test_large_decode_matches_oracle(cuda, large):
 
 
 def test_large_encode_matches_oracle(cuda, large):
-    """k_encode_lane output bytes == the oracle (== reference quicklz.c) for 1 MiB and 8 MiB;
-    the 50 MiB value is compressed on the GPU and round-tripped through the oracle decoder."""
+    """The whole-GPU encoder's output bytes == the oracle (== reference quicklz.c) for 1, 8 and
+    50 MiB values."""
     import torch
     from gobeansdb_amd import batch
     names = ["text_1MiB", "noisy_8MiB", "mixed_50MiB"]
@@ -156,3 +156,65 @@ def test_large_all_literal_and_periodic(cuda):
     torch.cuda.synchronize()
     assert st.cpu().numpy().tolist() == [0, 0, 0]
     assert out.to_bytes(dsz.cpu().numpy()) == plains
+
+
+def _encode_cases():
+    rng = np.random.default_rng(31)
+    return {
+        "zeros_300K": bytes(300_000),  # one bucket: hash_counter wraps every 256 positions (quicklz.c:316)
+        "period7_200K": (bytes(range(7)) * 40_000)[:200_000],
+        "random_100K": rng.integers(0, 256, 100_000, dtype=np.uint8).tobytes(),  # bails out: stored
+        "low6_150K": (rng.integers(0, 256, 150_000, dtype=np.uint8) & 0x3F).tobytes(),
+        "text_65537": O.gen_text(32, 0, 65537),
+        "text_70000": O.gen_text(33, 1, 70_000),
+        "noisy_3M": _noisy(34, 3 * MIB, 0.5),
+        "text_zero_text_2M": O.gen_text(35, 2, MIB) + bytes(50_000) + O.gen_text(35, 3, MIB),
+    }
+
+
+def test_large_encode_edge_cases_match_oracle(cuda):
+    """The whole-GPU encoder (qlzx_encode_huge.hip) on values just past 64 KiB, one-bucket data
+    (the hash counter's byte wrap), periodic and barely compressible data, a value that bails out
+    to stored, mixed with a small block in one batch; bytes == oracle/qlz_oracle.c (pinned to
+    quicklz.c), fused CRC of the output == crc32_write."""
+    import torch
+    from gobeansdb_amd import batch
+    cases = _encode_cases()
+    names = list(cases) + ["small"]
+    plains = [cases[k] for k in cases] + [O.gen_text(36, 0, 5000)]
+    src = batch.BlockBatch.from_bytes(plains)
+    dst, cs, st, crc = batch.compress(src, max_len=max(map(len, plains)),
+                                      crc_state=torch.full((len(plains),), -1, dtype=torch.int32, device="cuda"))
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().tolist() == [0] * len(plains)
+    outs = dst.to_bytes(cs.cpu().numpy())
+    for k, p, o, c in zip(names, plains, outs, crc.cpu().numpy().view(np.uint32)):
+        want = O.compress(p)
+        assert o == want, (k, len(o), len(want))
+        assert int(c) == O.crc32_write(0xFFFFFFFF, want) ^ 0xFFFFFFFF, k
+    assert outs[names.index("random_100K")][0] & 1 == 0  # stored
+
+
+def test_large_encode_go_compat_matches_oracle(cuda):
+    """QLZX_F_GO_COMPAT (Go quicklz.Compress, quicklz.go:80-289: the bail-out counts the header)
+    through the whole-GPU encoder == oracle compress_go."""
+    import torch
+    from gobeansdb_amd import batch
+    plains = [O.gen_text(37, 0, 90_000), bytes(200_000), _noisy(38, 400_000, 0.45)]
+    src = batch.BlockBatch.from_bytes(plains)
+    dst, cs, st, _ = batch.compress(src, go_compat=True, max_len=max(map(len, plains)))
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().tolist() == [0] * len(plains)
+    for p, o in zip(plains, dst.to_bytes(cs.cpu().numpy())):
+        assert o == O.compress_go(p)
+
+
+def test_large_single_call_compress(cuda):
+    """qlz_compress on a 6 MiB value (the per-call path over the batch encoder) == the oracle."""
+    import ctypes
+    from gobeansdb_amd import _lib
+    L = _lib.lib()
+    p = O.gen_text(39, 0, 6 * MIB)
+    out = ctypes.create_string_buffer(len(p) + 400)
+    n = L.qlz_compress(p, out, len(p), None)
+    assert out.raw[:n] == O.compress(p)

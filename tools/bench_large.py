@@ -6,7 +6,7 @@ decodes them (store/item.go:167).  Per size (1, 8, 50 MiB text values):
   * gpu_batch_decode_ms   qlzx_decompress_batch on a device-resident value (the whole-GPU path,
                           qlzx_decode_huge.hip), event time;
   * gpu_single_decode_ms  qlz_decompress from host memory (H2D + decode + D2H), wall time;
-  * gpu_batch_encode_ms / gpu_single_encode_ms   the same for compress;
+  * gpu_batch_encode_ms / gpu_single_encode_ms   the same for compress (qlzx_encode_huge.hip);
   * ref_decode_ms / ref_encode_ms   reference qlz_decompress / qlz_compress, one core.
 usage: python tools/bench_large.py [--out profiles/r04_large.json] [--reps 3]
 """
@@ -85,10 +85,27 @@ def main():
         if not a.no_encode:
             psrc = np.frombuffer(plain, np.uint8).copy()
             cdst = np.zeros(n + 400, np.uint8)
-            row["gpu_single_encode_ms"] = wall_ms(lambda: L.qlz_compress(psrc.ctypes.data, cdst.ctypes.data, n, None), 1)
+            r = L.qlz_compress(psrc.ctypes.data, cdst.ctypes.data, n, None)
+            assert cdst[:r].tobytes() == comp, "single-call encode differs from the oracle"
+            row["gpu_single_encode_ms"] = wall_ms(lambda: L.qlz_compress(psrc.ctypes.data, cdst.ctypes.data, n, None),
+                                                  a.reps)
+            pb = batch.BlockBatch.from_bytes([plain], device=dev)
+            cb = batch.BlockBatch.empty_for([n], device=dev, pad=400)
+            batch.compress(pb, cb, max_len=n, workspace=ws)
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(a.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                batch.compress(pb, cb, max_len=n, workspace=ws)
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            row["gpu_batch_encode_ms"] = round(float(np.median(ts)), 3)
             if ref is not None:
                 row["ref_encode_ms"] = wall_ms(lambda: ref[0].qlz_compress(psrc.ctypes.data, cdst.ctypes.data, n,
-                                                                           sc.ctypes.data), 1)
+                                                                           sc.ctypes.data), a.reps)
+                row["encode_speedup_vs_ref_1core"] = round(row["ref_encode_ms"] / row["gpu_single_encode_ms"], 2)
         rows.append(row)
         print(json.dumps(row), flush=True)
     res = {"what": "large text values: GPU decode/encode per value vs reference quicklz.c on one core",
