@@ -50,6 +50,10 @@ constexpr uint32_t kParseWG = 64;
 #define QLZX_CHUNK_BLOCKS 131072
 #endif
 constexpr uint32_t kChunkBlocks = QLZX_CHUNK_BLOCKS;  // >= 256 CUs x 8 waves x 64 lanes: K1 fills the chip
+#ifndef QLZX_FIRST_CHUNK  // the first chunk's K1 is not hidden under a K2: a smaller first chunk
+#define QLZX_FIRST_CHUNK QLZX_CHUNK_BLOCKS
+#endif
+constexpr uint32_t kFirstChunk = QLZX_FIRST_CHUNK < QLZX_CHUNK_BLOCKS ? QLZX_FIRST_CHUNK : QLZX_CHUNK_BLOCKS;
 #ifndef QLZX_K1_ROUND  // bytes per lane per DMA round: 32 (8 KiB ring per wave) measured best with the v4 K2
 #define QLZX_K1_ROUND 32
 #endif
@@ -418,7 +422,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     const bool sort = chunk > 64;
     // two workspace halves when the caller gave room for them: K1 of chunk c+1 runs on a
     // side stream while K2 of chunk c runs on `s` (K1 is latency-bound at low occupancy)
-    const bool overlap = ws_bytes >= 2 * one && b.n > chunk;
+    const bool overlap = ws_bytes >= 2 * one && b.n > kFirstChunk;
     // per host thread (the batch API is re-entrant like the reference) and per device: the
     // side stream and events are created on the device that owns `s`
     struct Side {  // destroyed with the thread (Go runs cgo calls on many OS threads)
@@ -475,8 +479,9 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
                            (uint32_t *)((uint8_t *)ws + o_list));
     }
     uint32_t c = 0;
-    for (uint32_t first = 0; first < b.n; first += chunk, c++) {
-        const uint32_t cnt = b.n - first < chunk ? b.n - first : chunk;
+    for (uint32_t first = 0, cnt = 0; first < b.n; first += cnt, c++) {
+        const uint32_t cap = c == 0 ? kFirstChunk : chunk;
+        cnt = b.n - first < cap ? b.n - first : cap;
         uint8_t *w = (uint8_t *)ws + (overlap ? (c & 1) * one : 0);
         BlkInfo *info = (BlkInfo *)w;
         GroupRec *recs = (GroupRec *)(w + o_rec);
