@@ -47,7 +47,7 @@ constexpr uint32_t kBlkSkip = 0, kBlkStored = 1, kBlkCompressed = 2;
 // K1 workgroup: one wave (the 16 KiB LDS ring per wave bounds occupancy)
 constexpr uint32_t kParseWG = 64;
 #ifndef QLZX_CHUNK_BLOCKS
-#define QLZX_CHUNK_BLOCKS 131072
+#define QLZX_CHUNK_BLOCKS 262144
 #endif
 constexpr uint32_t kChunkBlocks = QLZX_CHUNK_BLOCKS;  // >= 256 CUs x 8 waves x 64 lanes: K1 fills the chip
 #ifndef QLZX_FIRST_CHUNK  // the first chunk's K1 is not hidden under a K2: a smaller first chunk
