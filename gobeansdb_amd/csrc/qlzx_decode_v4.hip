@@ -292,6 +292,9 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse_g(qlzx_blocks b, const u
 #ifndef QLZX_K2_ASM_STORE
 #define QLZX_K2_ASM_STORE 0
 #endif
+#ifndef QLZX_K2_FARSEL
+#define QLZX_K2_FARSEL 1
+#endif
 #ifndef QLZX_K2_FARSPLIT
 #define QLZX_K2_FARSPLIT 0
 #endif
@@ -439,7 +442,13 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
         const bool wr = live && d < c + MR;
         if (wr) {
             L.mk[d & (MR - 1)] = key;
+#if QLZX_K2_FARSEL
+            // a match's own window slot holds a byte older than the far bound (d < c + MR) that no
+            // gather reads before the chunk of d overwrites it: the byte can go there unconditionally
+            L.win[d & (W - 1)] = (uint8_t)t;
+#else
             if (!ism) L.win[d & (W - 1)] = (uint8_t)t;
+#endif
         }
         pend = __ballot(live && !wr);
         pd = d;
@@ -579,9 +588,20 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
 #else
 #ifndef QLZX_EXP_NOFAR  // (timing experiment: far bytes read from the window, wrong output)
             if (__ballot(far)) {
+#if QLZX_K2_FARSEL
+                // every lane loads (a lane without a far byte reads the block's first output byte, which
+                // it ignores): no exec-mask branch per byte
+#pragma unroll
+                for (uint32_t j = 0; j < B; j++) {
+                    const bool fj = sv[j] < lo;
+                    const uint32_t x = dst[fj ? sv[j] : 0u];
+                    vb[j] = fj ? x : vb[j];
+                }
+#else
 #pragma unroll
                 for (uint32_t j = 0; j < B; j++)
                     if (sv[j] < lo) vb[j] = dst[sv[j]];
+#endif
             }
 #endif
 #pragma unroll
