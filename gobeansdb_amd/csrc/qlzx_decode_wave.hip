@@ -46,14 +46,21 @@ constexpr uint32_t kMaxDevices = 64;  // per-device side streams of the launcher
 constexpr uint32_t kBlkSkip = 0, kBlkStored = 1, kBlkCompressed = 2;
 // K1 workgroup: one wave (the 16 KiB LDS ring per wave bounds occupancy)
 constexpr uint32_t kParseWG = 64;
-#ifndef QLZX_CHUNK_BLOCKS
+#ifndef QLZX_CHUNK_BLOCKS  // blocks per K1/K2 chunk for batches of values up to 16 KiB
 #define QLZX_CHUNK_BLOCKS 262144
 #endif
-constexpr uint32_t kChunkBlocks = QLZX_CHUNK_BLOCKS;  // >= 256 CUs x 8 waves x 64 lanes: K1 fills the chip
-#ifndef QLZX_FIRST_CHUNK  // the first chunk's K1 is not hidden under a K2: a smaller first chunk
-#define QLZX_FIRST_CHUNK QLZX_CHUNK_BLOCKS
+#ifndef QLZX_CHUNK_BLOCKS_MIXED  // ... and for batches whose max_dsize exceeds 16 KiB
+#define QLZX_CHUNK_BLOCKS_MIXED 131072
 #endif
-constexpr uint32_t kFirstChunk = QLZX_FIRST_CHUNK < QLZX_CHUNK_BLOCKS ? QLZX_FIRST_CHUNK : QLZX_CHUNK_BLOCKS;
+// Chunk size by the call's max_dsize (>= 256 CUs x 8 waves x 64 lanes: K1 fills the chip).  Same-box
+// A/B (profiles/r04_c2_chunk_ab.txt, r04_chunk_c5_ab.txt): c2 (1 M x 16 KiB) 27.0 ms at 262144
+// vs 27.35 at 131072; c5 (mixed 4-64 KiB, 64 GiB) 549 GiB/s at 262144 vs 621 at 131072.
+__host__ __device__ inline uint32_t chunk_blocks(uint32_t max_dsize) {
+    return max_dsize <= 16384 ? (uint32_t)QLZX_CHUNK_BLOCKS : (uint32_t)QLZX_CHUNK_BLOCKS_MIXED;
+}
+__host__ __device__ inline uint32_t first_chunk_blocks(uint32_t max_dsize) {
+    return QLZX_FIRST_CHUNK < chunk_blocks(max_dsize) ? (uint32_t)QLZX_FIRST_CHUNK : chunk_blocks(max_dsize);
+}
 #ifndef QLZX_K1_ROUND  // bytes per lane per DMA round: 32 (8 KiB ring per wave) measured best with the v4 K2
 #define QLZX_K1_ROUND 32
 #endif
@@ -67,7 +74,8 @@ inline size_t rec_bytes_max(uint32_t md) { return (size_t)groups_max(md) * sizeo
 
 inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
     const uint32_t md = max_dsize > QLZX_FAST_MAX_DSIZE ? QLZX_FAST_MAX_DSIZE : max_dsize;
-    const uint32_t c = n < kChunkBlocks ? (n ? n : 1) : kChunkBlocks;
+    const uint32_t cb = chunk_blocks(max_dsize);
+    const uint32_t c = n < cb ? (n ? n : 1) : cb;
     return (((size_t)c * sizeof(BlkInfo) + 255) & ~(size_t)255) +
            ((((size_t)c * rec_bytes_max(md)) + 255) & ~(size_t)255) +
            ((((size_t)n * sizeof(uint32_t)) + 255) & ~(size_t)255) +              // block order, whole call
@@ -414,7 +422,8 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
                               hipStream_t s) {
     const uint32_t md = max_dsize > QLZX_FAST_MAX_DSIZE ? QLZX_FAST_MAX_DSIZE : max_dsize;
     const uint32_t gmax = groups_max(md);
-    const uint32_t chunk = b.n < kChunkBlocks ? b.n : kChunkBlocks;
+    const uint32_t chunk = b.n < chunk_blocks(max_dsize) ? b.n : chunk_blocks(max_dsize);
+    const uint32_t chunk0 = first_chunk_blocks(max_dsize);
     const size_t o_rec = ((size_t)chunk * sizeof(BlkInfo) + 255) & ~(size_t)255;
     const size_t one = decode_wave_ws_bytes(b.n, max_dsize);
     const size_t o_list = o_rec + ((((size_t)chunk * rec_bytes_max(md)) + 255) & ~(size_t)255);
@@ -422,7 +431,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     const bool sort = chunk > 64;
     // two workspace halves when the caller gave room for them: K1 of chunk c+1 runs on a
     // side stream while K2 of chunk c runs on `s` (K1 is latency-bound at low occupancy)
-    const bool overlap = ws_bytes >= 2 * one && b.n > kFirstChunk;
+    const bool overlap = ws_bytes >= 2 * one && b.n > chunk0;
     // per host thread (the batch API is re-entrant like the reference) and per device: the
     // side stream and events are created on the device that owns `s`
     struct Side {  // destroyed with the thread (Go runs cgo calls on many OS threads)
@@ -480,7 +489,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     }
     uint32_t c = 0;
     for (uint32_t first = 0, cnt = 0; first < b.n; first += cnt, c++) {
-        const uint32_t cap = c == 0 ? kFirstChunk : chunk;
+        const uint32_t cap = c == 0 ? chunk0 : chunk;
         cnt = b.n - first < cap ? b.n - first : cap;
         uint8_t *w = (uint8_t *)ws + (overlap ? (c & 1) * one : 0);
         BlkInfo *info = (BlkInfo *)w;
