@@ -58,6 +58,9 @@ constexpr uint32_t kParseWG = 64;
 __host__ __device__ inline uint32_t chunk_blocks(uint32_t max_dsize) {
     return max_dsize <= 16384 ? (uint32_t)QLZX_CHUNK_BLOCKS : (uint32_t)QLZX_CHUNK_BLOCKS_MIXED;
 }
+#ifndef QLZX_FIRST_CHUNK  // the first chunk's K1 is not hidden under a K2: a smaller first chunk (measured no gain)
+#define QLZX_FIRST_CHUNK 0xffffffffu
+#endif
 __host__ __device__ inline uint32_t first_chunk_blocks(uint32_t max_dsize) {
     return QLZX_FIRST_CHUNK < chunk_blocks(max_dsize) ? (uint32_t)QLZX_FIRST_CHUNK : chunk_blocks(max_dsize);
 }
