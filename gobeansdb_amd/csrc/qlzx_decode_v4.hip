@@ -292,8 +292,11 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse_g(qlzx_blocks b, const u
 #ifndef QLZX_K2_ASM_STORE
 #define QLZX_K2_ASM_STORE 0
 #endif
-#ifndef QLZX_K2_FARSEL
+#ifndef QLZX_K2_FARSEL  // literal window byte written for every item that marks (no nested branch)
 #define QLZX_K2_FARSEL 1
+#endif
+#ifndef QLZX_K2_FARALL  // far loads issued by every lane of a chunk with far bytes
+#define QLZX_K2_FARALL 0
 #endif
 #ifndef QLZX_K2_FARSPLIT
 #define QLZX_K2_FARSPLIT 0
@@ -588,15 +591,18 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
 #else
 #ifndef QLZX_EXP_NOFAR  // (timing experiment: far bytes read from the window, wrong output)
             if (__ballot(far)) {
-#if QLZX_K2_FARSEL
+#if QLZX_K2_FARALL
                 // every lane loads (a lane without a far byte reads the block's first output byte, which
-                // it ignores): no exec-mask branch per byte
+                // it ignores): no exec-mask branch per byte -- measured slower (27.2 vs 27.0 ms on c2):
+                // the loads of lanes without far bytes cost more than the branches they save
+                uint32_t x[B];
 #pragma unroll
-                for (uint32_t j = 0; j < B; j++) {
-                    const bool fj = sv[j] < lo;
-                    const uint32_t x = dst[fj ? sv[j] : 0u];
-                    vb[j] = fj ? x : vb[j];
-                }
+                for (uint32_t j = 0; j < B; j++) x[j] = dst[sv[j] < lo ? sv[j] : 0u];
+                // one barrier over all loads keeps them out of per-byte branches and in flight together
+#pragma unroll
+                for (uint32_t h = 0; h < B; h += 4) asm volatile("" : "+v"(x[h]), "+v"(x[h + 1]), "+v"(x[h + 2]), "+v"(x[h + 3]));
+#pragma unroll
+                for (uint32_t j = 0; j < B; j++) vb[j] = sv[j] < lo ? x[j] : vb[j];
 #else
 #pragma unroll
                 for (uint32_t j = 0; j < B; j++)
