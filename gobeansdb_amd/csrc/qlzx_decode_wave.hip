@@ -64,6 +64,12 @@ __host__ __device__ inline uint32_t chunk_blocks(uint32_t max_dsize) {
 __host__ __device__ inline uint32_t first_chunk_blocks(uint32_t max_dsize) {
     return QLZX_FIRST_CHUNK < chunk_blocks(max_dsize) ? (uint32_t)QLZX_FIRST_CHUNK : chunk_blocks(max_dsize);
 }
+#ifndef QLZX_K1_NOMAT2  // K1 steps take one match at most (no second match from the same dword)
+#define QLZX_K1_NOMAT2 0
+#endif
+#ifndef QLZX_K1_MLATE  // a group's match bits taken from its control word when it is recorded
+#define QLZX_K1_MLATE 1
+#endif
 #ifndef QLZX_K1_ROUND  // bytes per lane per DMA round: 32 (8 KiB ring per wave) measured best with the v4 K2
 #define QLZX_K1_ROUND 32
 #endif
@@ -289,14 +295,23 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
             // a second match right after it when its first byte is already in w
             const uint32_t ip2 = ipm + code + 1, k2 = km + 1;
             const uint32_t w2 = w >> (8 * ((code + 1) & 3));
+#if QLZX_K1_NOMAT2
+            const bool mat2 = false;
+#else
             const bool mat2 = mat & (code < 3) & (k2 < 31) & (((cw >> (k2 & 31)) & 1u) != 0) & (ip2 < csize) &
                               (ip2 + 1 <= lim);
+#endif
             const uint32_t ty2 = (w2 & 3u) + ((w2 & 127u) == 3u ? 1u : 0u);
             const uint32_t code2 = __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4);
             bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) |  // C1, group bound
                                    (mat & (ipm + code + 1 > csize)) |        // C2
                                    (mat2 & (ip2 + code2 + 1 > csize)));
+#if QLZX_K1_MLATE
+            // a group's match bits are its control word's (every item of a finished group is parsed)
+            if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, cw & 0x7fffffffu, ra, rb};
+#else
             if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
+#endif
             st = bad ? QLZX_E_CORRUPT : st;
             const bool adv = stepping & !bad;
             const bool ag = adv & gb;
@@ -307,7 +322,9 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
             g += ag ? 1u : 0u;
             ip += adv ? (gb ? 4u : run + (mat ? code + 1 : 0u) + (mat2 ? code2 + 1 : 0u)) : 0u;
             k = adv ? (gb ? 0u : km + (mat ? 1u : 0u) + (mat2 ? 1u : 0u)) : k;
+#if !QLZX_K1_MLATE
             m = adv ? (gb ? 0u : m | bm | bm2) : m;
+#endif
             ra = adv ? (gb ? 0u : ra | ((code & 1u) ? bm : 0u) | ((code2 & 1u) ? bm2 : 0u)) : ra;
             rb = adv ? (gb ? 0u : rb | ((code & 2u) ? bm : 0u) | ((code2 & 2u) ? bm2 : 0u)) : rb;
             done_parse = done_parse | (go & (end | bad));
@@ -319,7 +336,12 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
         ring_issue(ring, gbase, dummy, r + 3, last16, stream && r + 3 <= last_round);
     }
     PROF_MARK(4);  // 4: DMA issue + loop overhead
+#if QLZX_K1_MLATE
+    if (parsing && st == QLZX_OK && g > 0)  // the last group: its first k items
+        myrec[g - 1] = GroupRec{rec_ip, cw & (k >= 31 ? 0x7fffffffu : ((1u << k) - 1u)), ra, rb};
+#else
     if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
+#endif
     PROF_FLUSH(0);
     vm_sync();
     if (!inrange) return;
