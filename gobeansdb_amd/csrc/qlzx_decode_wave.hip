@@ -243,7 +243,10 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uin
     const bool parsing = stream && st == QLZX_OK && kind == kBlkCompressed;
 
     // parse state
-    uint32_t ip = hdr, g = 0, k = 31, cw = 0, m = 0, ra = 0, rb = 0, rec_ip = 0;
+    uint32_t ip = hdr, g = 0, k = 31, cw = 0, ra = 0, rb = 0, rec_ip = 0;
+#if !QLZX_K1_MLATE
+    uint32_t m = 0;
+#endif
     GroupRec *myrec = recs + (size_t)(inrange ? lin : 0) * gmax;
     bool done_parse = !parsing;
 

@@ -15,6 +15,7 @@
 // Launches rotate over kSvcStreams streams, so a batch launched while an earlier one still runs
 // does not queue behind it.  Values above kSvcMaxLen (and the Go-compat encoder modes) take the
 // general per-call path in qlzx_api.hip.
+#include <chrono>
 #include <thread>
 #include <vector>
 #include <immintrin.h>
@@ -24,6 +25,10 @@ namespace qlzx {
 constexpr uint32_t kSvcSlots = 64;        // concurrent requests (pinned + device arena)
 constexpr uint32_t kSvcBatchMax = 32;     // requests per launch (kernel-argument descriptor)
 constexpr uint32_t kSvcStreams = 4;
+// Coalescing: with requests already on the GPU, a new batch waits for kSvcBatchTarget requests or
+// kSvcDeadlineNs, whichever comes first (a lone caller finds nothing in flight and launches at once).
+constexpr uint32_t kSvcBatchTarget = 8;
+constexpr int64_t kSvcDeadlineNs = 20000;
 constexpr uint32_t kSvcMaxLen = 65536;    // dsize / input length served here (solo decoder, WG encoder)
 constexpr size_t kSvcIn = 80u << 10, kSvcOut = 80u << 10;
 constexpr size_t kSvcHostSlot = kSvcIn + kSvcOut;
@@ -148,6 +153,11 @@ using qlzx::kSvcBatchMax;
 using qlzx::kSvcSlots;
 using qlzx::kSvcStreams;
 
+inline int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
 struct SvcPending {
     uint32_t op;
     qlzx::SvcReq r;
@@ -167,6 +177,8 @@ struct Service {
     std::vector<SvcPending> pending;
     std::atomic<bool> leading{false};
     std::atomic<uint32_t> npending{0};
+    std::atomic<uint32_t> inflight{0};     // launched, completion not yet seen by the caller
+    std::atomic<int64_t> oldest_ns{0};     // when the oldest pending request was queued
     uint32_t next_stream = 0;
 
     int init(int device) {
@@ -240,12 +252,16 @@ struct Service {
         volatile qlzx::SvcDone *d = h_done + r.slot;
         {
             std::lock_guard<std::mutex> g(mu);
+            if (pending.empty()) oldest_ns.store(now_ns(), std::memory_order_relaxed);
             pending.push_back({op, r});
             npending.fetch_add(1, std::memory_order_release);
         }
         int rc = QLZX_R_OK;
         for (uint32_t spins = 0; d->seq != r.seq; spins++) {
-            if (!leading.load(std::memory_order_acquire) && npending.load(std::memory_order_acquire)) {
+            const uint32_t np = npending.load(std::memory_order_acquire);
+            if (!leading.load(std::memory_order_acquire) && np &&
+                (inflight.load(std::memory_order_acquire) == 0 || np >= qlzx::kSvcBatchTarget ||
+                 now_ns() - oldest_ns.load(std::memory_order_relaxed) > qlzx::kSvcDeadlineNs)) {
                 bool exp = false;
                 if (leading.compare_exchange_strong(exp, true, std::memory_order_acq_rel)) {
                     std::vector<SvcPending> batch;
@@ -255,6 +271,8 @@ struct Service {
                         batch.assign(pending.begin(), pending.begin() + n);
                         pending.erase(pending.begin(), pending.begin() + n);
                         npending.fetch_sub((uint32_t)n, std::memory_order_release);
+                        inflight.fetch_add((uint32_t)n, std::memory_order_acq_rel);
+                        if (!pending.empty()) oldest_ns.store(now_ns(), std::memory_order_relaxed);
                     }
                     const int lr = batch.empty() ? QLZX_R_OK : launch(batch);
                     if (lr != QLZX_R_OK) {
@@ -272,6 +290,7 @@ struct Service {
             if (spins > 20000) std::this_thread::yield(); else _mm_pause();
         }
         std::atomic_thread_fence(std::memory_order_acquire);
+        inflight.fetch_sub(1, std::memory_order_acq_rel);
         if (d->status == -1 && rc == QLZX_R_OK) rc = fail(QLZX_R_HIP, "service launch failed (another caller's batch)");
         return rc;
     }
