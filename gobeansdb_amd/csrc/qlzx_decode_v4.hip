@@ -24,6 +24,12 @@
 #ifndef QLZX_K1_STRUCT
 #define QLZX_K1_STRUCT 0
 #endif
+#ifndef QLZX_K1_V4M2  // k_dec_parse4 takes a second match from the same dword, as k_dec_parse does
+#define QLZX_K1_V4M2 1
+#endif
+#ifndef QLZX_K1_V4M3  // ... or up to three matches from an 8-byte window
+#define QLZX_K1_V4M3 0
+#endif
 namespace qlzx {
 
 // ------------------------------------------------------------------------------- K1 ----
@@ -144,15 +150,57 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
             const uint32_t w = ring_rd32(ring, q + shift, lane);
             const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
             const uint32_t e = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);  // token bytes - 1
+#if QLZX_K1_V4M3
+            // up to three matches per step from an 8-byte window at q (the tokens' first bytes)
+            const uint32_t wh = ring_rd32(ring, q + 4 + shift, lane);
+            const uint64_t W8 = ((uint64_t)wh << 32) | w;
+            const uint32_t q2 = q + e + 1, rest2 = rest >> 1;
+            const bool hasm2 = hasm & ((rest2 & 1u) != 0) & (rest2 != 1u) & (q2 < csize) & (q2 + 1 <= lim);
+            const uint32_t t2 = (uint32_t)(W8 >> (8 * (e + 1)));
+            const uint32_t ty2 = (t2 & 3u) + ((t2 & 127u) == 3u ? 1u : 0u);
+            const uint32_t e2 = hasm2 ? __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4) : 0u;
+            const uint32_t q3 = q2 + e2 + 1, rest3 = rest2 >> 1;
+            const bool hasm3 = hasm2 & ((rest3 & 1u) != 0) & (rest3 != 1u) & (q3 < csize) & (q3 + 1 <= lim) &
+                               (e + e2 + 2 <= 7u);
+            const uint32_t t3 = (uint32_t)(W8 >> (8 * ((e + e2 + 2) & 7u)));
+            const uint32_t ty3 = (t3 & 3u) + ((t3 & 127u) == 3u ? 1u : 0u);
+            const uint32_t e3 = hasm3 ? __builtin_amdgcn_ubfe(0x32110u, ty3 * 4, 4) : 0u;
+            const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) | (hasm & (q2 > csize)) |
+                                         (hasm2 & (q3 > csize)) | (hasm3 & (q3 + e3 + 1 > csize)));
+#elif QLZX_K1_V4M2
+            // a second match right after the first when its first byte is already in w
+            const uint32_t q2 = q + e + 1, rest2 = rest >> 1;
+            const bool hasm2 = hasm & (e < 3u) & ((rest2 & 1u) != 0) & (rest2 != 1u) & (q2 < csize) & (q2 + 1 <= lim);
+            const uint32_t w2 = w >> (8 * ((e + 1) & 3u));
+            const uint32_t ty2 = (w2 & 3u) + ((w2 & 127u) == 3u ? 1u : 0u);
+            const uint32_t e2 = hasm2 ? __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4) : 0u;
+            const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) | (hasm & (q2 > csize)) |
+                                         (hasm2 & (q2 + e2 + 1 > csize)));
+#else
             const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) | (hasm & (q + e + 1 > csize)));
+#endif
             if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, cwg, ra, rb};
             st = bad ? QLZX_E_CORRUPT : st;
             const bool adv = stepping & !bad;
             const uint32_t kb = hasm ? 1u << (__builtin_clz(cwr) + run) : 0u;  // item index clz(cwr) + run
+#if QLZX_K1_V4M3
+            const uint32_t kb2 = hasm2 ? kb << 1 : 0u, kb3 = hasm3 ? kb << 2 : 0u;
+            const uint32_t nip = gb ? ip + 4 : q + (hasm ? e + 1 : 0u) + (hasm2 ? e2 + 1 : 0u) + (hasm3 ? e3 + 1 : 0u);
+            const uint32_t ncwr = gb ? w : (rest >> (hasm ? (hasm2 ? (hasm3 ? 3 : 2) : 1) : 0));
+            const uint32_t nra = gb ? 0u : (ra | ((e & 1u) ? kb : 0u) | ((e2 & 1u) ? kb2 : 0u) | ((e3 & 1u) ? kb3 : 0u));
+            const uint32_t nrb = gb ? 0u : (rb | ((e & 2u) ? kb : 0u) | ((e2 & 2u) ? kb2 : 0u) | ((e3 & 2u) ? kb3 : 0u));
+#elif QLZX_K1_V4M2
+            const uint32_t kb2 = hasm2 ? kb << 1 : 0u;
+            const uint32_t nip = gb ? ip + 4 : q + (hasm ? e + 1 : 0u) + (hasm2 ? e2 + 1 : 0u);
+            const uint32_t ncwr = gb ? w : (rest >> (hasm ? (hasm2 ? 2 : 1) : 0));
+            const uint32_t nra = gb ? 0u : (ra | ((e & 1u) ? kb : 0u) | ((e2 & 1u) ? kb2 : 0u));
+            const uint32_t nrb = gb ? 0u : (rb | ((e & 2u) ? kb : 0u) | ((e2 & 2u) ? kb2 : 0u));
+#else
             const uint32_t nip = gb ? ip + 4 : q + (hasm ? e + 1 : 0u);
             const uint32_t ncwr = gb ? w : (rest >> (hasm ? 1 : 0));
             const uint32_t nra = gb ? 0u : (ra | ((e & 1u) ? kb : 0u));
             const uint32_t nrb = gb ? 0u : (rb | ((e & 2u) ? kb : 0u));
+#endif
             rec_ip = (adv & gb) ? ip : rec_ip;
             cwg = (adv & gb) ? w : cwg;
             g += (adv & gb) ? 1u : 0u;

@@ -431,7 +431,7 @@ constexpr uint32_t kWinB = QLZX_K2B_WIN, kMarkRing = QLZX_K2B_MR;
 #define QLZX_K1_GLOBAL 0
 #endif
 #ifndef QLZX_K1_V3  // the round-3 K1 (a literal run and up to two matches per step) in front of the v4 K2
-#define QLZX_K1_V3 1
+#define QLZX_K1_V3 0
 #endif
 namespace qlzx {
 
