@@ -340,6 +340,9 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse_g(qlzx_blocks b, const u
 #ifndef QLZX_K2_ASM_STORE
 #define QLZX_K2_ASM_STORE 0
 #endif
+#ifndef QLZX_K2_COUNTED  // chunk loop with its trip count computed at entry
+#define QLZX_K2_COUNTED 0
+#endif
 #ifndef QLZX_K2_FARSEL  // literal window byte written for every item that marks (no nested branch)
 #define QLZX_K2_FARSEL 1
 #endif
@@ -514,7 +517,15 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
 
     // chunk phases while every item starting below c + 256 is known; true when the block is done
     auto chunks = [&]() __attribute__((always_inline)) -> bool {
+#if QLZX_K2_COUNTED
+        // D does not move while chunks run: the number of ready chunks is known up front
+        const uint32_t left = c < dsize ? (dsize - c + CH - 1) / CH : 0u;
+        uint32_t nch = complete ? left : (D >= c + CH ? min((D - c) / CH, left) : 0u);
+        nch = __builtin_amdgcn_readfirstlane(nch);
+        for (; nch; nch--) {
+#else
         while (c < dsize && (complete || D >= c + CH)) {
+#endif
             if (pend) {  // items of the last batch that start at or above c_prev + MR
                 const bool wr = ((pend >> lane) & 1u) && pd < c + MR;
                 if (wr) {
