@@ -475,7 +475,7 @@ def bench_compress(args, rank, world, dev, kind, emit: bool = True):
     achieved = (n * bs + csum) / (kern_ms * 1e-3) / 1e9
     traffic = None
     traffic_src = None
-    tj = args.traffic_json or os.path.join(ROOT, "profiles", "r03_c3_traffic.json")
+    tj = args.traffic_json or os.path.join(ROOT, "profiles", "r04_c3_traffic.json")
     if os.path.exists(tj) and kind == "image" and bs == 65536:
         tpb = json.load(open(tj))["hbm_bytes_per_block"]
         traffic = round(tpb * n)
