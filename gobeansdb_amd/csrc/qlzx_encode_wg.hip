@@ -165,11 +165,28 @@ constexpr uint32_t kEncGroups = 256;  // bucket groups (hash >> 4), 16 buckets e
 #ifndef QLZX_ENC_SPEC_COPY
 #define QLZX_ENC_SPEC_COPY 1
 #endif
-#ifndef QLZX_ENC_CAND_LDS
-#define QLZX_ENC_CAND_LDS 1
-#endif
 #ifndef QLZX_ENC_PREFIX
 #define QLZX_ENC_PREFIX 1
+#endif
+// Radix scatter: a lane's same-key peers from one 64-bit LDS OR per lane into a per-wave key slot
+// (read back, then cleared) instead of one ballot per key bit.
+#ifndef QLZX_ENC_LDS_PEERS
+#define QLZX_ENC_LDS_PEERS 0
+#endif
+// Best match in poorly compressible blocks (3-gram repeats, the stored proof's D, below
+// QLZX_ENC_COMPACT_PCT % of the positions; 0 = never): a wave whose lanes all have at most
+// kMatchCompactMax candidates that can match (same 3 bytes, far enough back) visits only those,
+// in a per-lane bit loop, instead of all 16.
+#ifndef QLZX_ENC_COMPACT_PCT
+#define QLZX_ENC_COMPACT_PCT 60
+#endif
+#ifndef QLZX_ENC_MATCH_COMPACT
+#define QLZX_ENC_MATCH_COMPACT 10
+#endif
+constexpr uint32_t kMatchCompactMax = QLZX_ENC_MATCH_COMPACT;
+// Bucket starts of the 64 KiB kernel in LDS (8 KiB) rather than in the workgroup's global slot.
+#ifndef QLZX_ENC_BST_LDS
+#define QLZX_ENC_BST_LDS 1
 #endif
 constexpr uint32_t kPrefixMinLen = QLZX_ENC_PREFIX ? 16384 : 0xFFFFFFFFu, kPrefixRepeatPct = 28, kPrefixMargin = 1024;
 constexpr uint32_t kParseRounds = 4;  // segment-walker rounds before the serial item walk
@@ -194,10 +211,11 @@ __device__ __forceinline__ uint32_t cslot(uint32_t L) {
 }
 constexpr uint32_t cslots(uint32_t nkeys, uint32_t W) { return nkeys * (W + 1); }
 
-template <uint32_t W, uint32_t NB_LOG2, typename OUT>
+//   pe        (LP) per-wave 256-slot u64 LDS array, all zero on entry and on exit
+template <uint32_t W, uint32_t NB_LOG2, bool LP, typename OUT>
 __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t *in, OUT *out, uint32_t shift,
                                  uint32_t *cnt, uint64_t *wsum, unsigned long long *sub, uint32_t *hist,
-                                 uint32_t *next_cnt, bool counted) {
+                                 uint32_t *next_cnt, bool counted, unsigned long long *pe) {
 #ifdef QLZX_PROFILE
 #define SUB_MARK(k)                                                         \
     do {                                                                    \
@@ -278,7 +296,17 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
         const uint32_t f = fetch24(s_in, p);
         const uint32_t h = hash12(f);
         const uint32_t key = valid ? (h >> shift) & (NB - 1) : 0u;
-        const uint64_t peers = match_peers<NB_LOG2>(key, __ballot(valid));
+        uint64_t peers;
+        if constexpr (LP) {
+            // in-order LDS per wave: every lane's OR lands before any lane's read, every read
+            // before any lane's clear
+            unsigned long long *ps = pe + wave * 256 + key;
+            if (valid) __hip_atomic_fetch_or(ps, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            peers = valid ? *(volatile unsigned long long *)ps : 0ull;
+            if (valid) *(volatile unsigned long long *)ps = 0ull;
+        } else {
+            peers = match_peers<NB_LOG2>(key, __ballot(valid));
+        }
         const uint32_t intra = __popcll(peers & ltm);
         uint32_t cur = 0;
         if (valid) cur = cnt[cslot<W>(key * W + wave)];
@@ -299,17 +327,22 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
 // plus bst[h] = the sorted index where bucket h starts (exclusive scan of the
 // bucket histogram counted in the first pass).  tmp: u16[P] scratch; s_hist:
 // 2048 words of LDS free during the sort; s_cnt: 272 * (W + 1) words.
-template <uint32_t W>
+template <uint32_t W, uint32_t L8_BYTES>
 __device__ void bucket_sort(const uint8_t *s_in, uint32_t P, uint16_t *tmp, uint32_t *gl, uint16_t *bst,
                             uint32_t *s_cnt, uint32_t *s_hist, uint64_t *wsum, unsigned long long *subA,
                             unsigned long long *subB) {
     constexpr uint32_t T = 64 * W;
     const uint32_t tid = tid_here();
     uint32_t *cntB = s_cnt, *cntA = s_cnt + cslots(kEncGroups, W);
+    // LDS peer slots after the histogram, where the workgroup's LDS has room for them
+    constexpr bool LP = QLZX_ENC_LDS_PEERS && L8_BYTES >= QLZX_BUCKETS * 2 + W * 256 * 8;
+    unsigned long long *pe = (unsigned long long *)(s_hist + QLZX_BUCKETS / 2);
+    if constexpr (LP)
+        for (uint32_t k = tid; k < W * 256; k += T) pe[k] = 0ull;
     for (uint32_t k = tid; k < QLZX_BUCKETS / 2; k += T) s_hist[k] = 0;
     for (uint32_t k = tid; k < cslots(kEncGroups, W); k += T) cntB[k] = 0;
     // (pass A zeroes its own counters and syncs before counting)
-    stable_partition<W, 4>(s_in, P, nullptr, tmp, 0, cntA, wsum, subA, s_hist, cntB, false);
+    stable_partition<W, 4, LP>(s_in, P, nullptr, tmp, 0, cntA, wsum, subA, s_hist, cntB, false, pe);
     // bucket starts: exclusive scan of the u16-pair histogram, bucket order = sorted order
     {
         constexpr uint32_t PT = QLZX_BUCKETS / 2 / T > 0 ? QLZX_BUCKETS / 2 / T : 1;  // words per thread
@@ -334,7 +367,7 @@ __device__ void bucket_sort(const uint8_t *s_in, uint32_t P, uint16_t *tmp, uint
 #ifdef QLZX_PROFILE
     if (subB) subB[7] = __builtin_amdgcn_s_memtime();
 #endif
-    stable_partition<W, 8>(s_in, P, tmp, gl, 4, cntB, wsum, subB, nullptr, nullptr, true);
+    stable_partition<W, 8, LP>(s_in, P, tmp, gl, 4, cntB, wsum, subB, nullptr, nullptr, true, pe);
 }
 
 template <uint32_t CAP>
@@ -375,11 +408,13 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
     __shared__ __attribute__((aligned(16))) uint32_t s_scr[C::SCR];
     __shared__ uint64_t s_wsum[W];
     __shared__ uint32_t s_misc[24];  // [0] next group, [1] proof count, [4..] CRC stripes
+    constexpr bool BL = QLZX_ENC_BST_LDS && CAP == 65536;  // (the smaller kernels' occupancy is LDS-bound)
+    __shared__ uint16_t s_bst[BL ? QLZX_BUCKETS : 1];
     uint8_t *const s_in = s_u, *const s_l8 = s_u + C::IN_B;
 
     uint32_t *gl = (uint32_t *)(ws + (size_t)blockIdx.x * C::SLOT_BYTES);
     uint16_t *goff = (uint16_t *)(gl + CAP);
-    uint16_t *bst = goff + CAP;  // sorted-list start of each bucket
+    uint16_t *bst = BL ? s_bst : goff + CAP;  // sorted-list start of each bucket
 
     PROF_DECL
 #ifdef QLZX_PROFILE
@@ -408,6 +443,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
         }
         bool stored = false;
         bool prefix = false;  // try the prefix-only pass first (below, phase 4)
+        bool cmode = false;   // compact best-match loop (phase 2)
 
         PROF_MARK(0);  // 0: ticket + setup
         QLZX_TID_REFRESH();
@@ -497,6 +533,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             // poorly compressible but not provably stored (the c3 noisy blocks): likely to bail out
             // at the first control word past 3/4 of the input, so try the prefix alone first
             prefix = !stored && n >= kPrefixMinLen && 100ull * (ny - s_misc[1]) < (uint64_t)kPrefixRepeatPct * ny;
+            cmode = !stored && 100ull * (ny - s_misc[1]) < (uint64_t)QLZX_ENC_COMPACT_PCT * ny;
             if (stored) {  // quicklz.c:722-727 from the global copy of the input
                 QLZX_TID_REFRESH();
                 if ((((uintptr_t)dst) & 15u) == 0) {
@@ -565,7 +602,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
 #else
                 unsigned long long *subA = nullptr, *subB = nullptr;
 #endif
-                bucket_sort<W>(s_in, P, goff, gl, bst, s_scr, (uint32_t *)s_l8, s_wsum, subA, subB);
+                bucket_sort<W, C::L8_B>(s_in, P, goff, gl, bst, s_scr, (uint32_t *)s_l8, s_wsum, subA, subB);
 
                 PROF_MARK(2);  // 2: sort by bucket
                 QLZX_TID_REFRESH();
@@ -576,7 +613,6 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 // Longest wins, ties to the larger position (quicklz.c:344): scanning from
                 // the most recent, a candidate must be strictly longer, and a match of the
                 // full extension limit ends the scan.
-#if QLZX_ENC_CAND_LDS
                 // The candidates of the wave's 64 consecutive sorted indices are the 16 entries
                 // before the first and the wave's own: each list entry is loaded from global
                 // memory once per wave-iteration into an 80-word LDS stage (s_scr is free between
@@ -584,7 +620,8 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 // of consecutive words, not 16 global loads.
                 static_assert(C::SCR >= 80 * W, "candidate stage");
                 uint32_t *stg = s_scr + wave * 80;
-                for (uint32_t t0 = tid - lane; t0 < P; t0 += T) {  // wave-uniform
+                auto best_matches = [&](auto compact) {
+                  for (uint32_t t0 = tid - lane; t0 < P; t0 += T) {  // wave-uniform
                     const uint32_t t = t0 + lane;
                     const bool act = t < P;
                     const uint32_t self = act ? gl[t] : 0u;
@@ -595,31 +632,15 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     const uint32_t p = self & 0xFFFFu, fh = self >> 16;
                     const uint32_t rm = (t - (uint32_t)bst[hash12(fetch24(s_in, p))]) & 255u;
                     const uint32_t d = rm < 16u ? rm : 16u;
-                    uint32_t cand[16];  // most recent first
-#pragma unroll
-                    for (uint32_t k = 0; k < 16; k++) cand[k] = stg[k < d ? 15u + lane - k : 16u + lane];
-#else
-                for (uint32_t t = tid; t < P; t += T) {
-                    const uint32_t self = gl[t], p = self & 0xFFFFu, fh = self >> 16;
-                    const uint32_t rm = (t - (uint32_t)bst[hash12(fetch24(s_in, p))]) & 255u;
-                    const uint32_t d = rm < 16u ? rm : 16u;
-                    uint32_t cand[16];  // most recent first; all 16 loads in flight at once
-#pragma unroll
-                    for (uint32_t k = 0; k < 16; k++) cand[k] = gl[k < d ? t - 1 - k : t];
-#endif
                     const uint32_t limit = min(255u, n - 4u - p);  // quicklz.c:310
-                    // First pass: bytes 3..6 of every candidate against this position's, all 16
+                    // First pass: bytes 3..6 of every candidate against this position's, all
                     // LDS reads independent.  A mismatch there gives the exact length; the
                     // candidates equal through byte 6 ("long") are extended afterwards, most
                     // recent first -- they beat every short one, and ties stay with the more
                     // recent (larger) position.
                     const uint32_t P3 = ld32u(s_in, p + 3);
                     uint32_t best = 0, bpos = 0, longm = 0;
-#pragma unroll
-                    for (uint32_t k = 0; k < 16; k++) {
-                        const uint32_t q = cand[k] & 0xFFFFu;
-                        // same bucket + same fetch[23:12] = same 3 bytes; o < src - MINOFFSET
-                        const bool ok = k < d && (cand[k] >> 16) == fh && q + 3u <= p;
+                    auto first = [&](uint32_t k, uint32_t q, bool ok) {
                         const uint32_t x = ld32u(s_in, q + 3) ^ P3;
                         const uint32_t m = min(x ? 3u + ((uint32_t)__builtin_ctz(x) >> 3) : 7u, limit);
                         if (ok && !x && limit > 7u) longm |= 1u << k;
@@ -627,16 +648,41 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                             best = m;
                             bpos = q;
                         }
+                    };
+                    if constexpr (decltype(compact)::value) {
+                        // candidates that can match: same bucket + same fetch[23:12] = same 3
+                        // bytes, o < src - MINOFFSET (stage words past d: masked)
+                        uint32_t okm = 0;
+#pragma unroll
+                        for (uint32_t k = 0; k < 16; k++) {
+                            const uint32_t c = stg[15u + lane - k];
+                            okm |= (k < d && (c >> 16) == fh && (c & 0xFFFFu) + 3u <= p) ? 1u << k : 0u;
+                        }
+                        if (__ballot((uint32_t)__popc(okm) > kMatchCompactMax) == 0ull) {  // wave-uniform
+                            for (uint32_t t2 = okm; t2; t2 &= t2 - 1u) {  // set bits, most recent first
+                                const uint32_t k = (uint32_t)__builtin_ctz(t2);
+                                first(k, stg[15u + lane - k] & 0xFFFFu, true);
+                            }
+                        } else {
+#pragma unroll
+                            for (uint32_t k = 0; k < 16; k++) first(k, stg[15u + lane - k] & 0xFFFFu, (okm >> k) & 1u);
+                        }
+                    } else {
+                        uint32_t cand[16];  // most recent first
+#pragma unroll
+                        for (uint32_t k = 0; k < 16; k++) cand[k] = stg[k < d ? 15u + lane - k : 16u + lane];
+#pragma unroll
+                        for (uint32_t k = 0; k < 16; k++) {
+                            const uint32_t q = cand[k] & 0xFFFFu;
+                            // same bucket + same fetch[23:12] = same 3 bytes; o < src - MINOFFSET
+                            first(k, q, k < d && (cand[k] >> 16) == fh && q + 3u <= p);
+                        }
                     }
                     if (longm) best = 0;  // a long candidate always wins
                     while (longm && best < limit) {
                         const uint32_t k = (uint32_t)__builtin_ctz(longm);
                         longm &= longm - 1u;
-#if QLZX_ENC_CAND_LDS
                         const uint32_t q = stg[15u + lane - k] & 0xFFFFu;
-#else
-                        const uint32_t q = gl[t - 1 - k] & 0xFFFFu;
-#endif
                         uint32_t m = 7;
                         for (;;) {
                             const uint32_t x = ld32u(s_in, q + m) ^ ld32u(s_in, p + m);
@@ -655,7 +701,10 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     }
                     s_l8[p] = (uint8_t)best;  // 0 = literal, else 3..255
                     if (best) goff[p] = (uint16_t)(p - bpos);
-                }
+                  }
+                };
+                if (cmode) best_matches(std::true_type{});
+                else best_matches(std::false_type{});
             }
             __syncthreads();
 
