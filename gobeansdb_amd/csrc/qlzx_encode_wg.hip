@@ -184,6 +184,20 @@ constexpr uint32_t kEncGroups = 256;  // bucket groups (hash >> 4), 16 buckets e
 #define QLZX_ENC_MATCH_COMPACT 10
 #endif
 constexpr uint32_t kMatchCompactMax = QLZX_ENC_MATCH_COMPACT;
+// Bail-out after a parse: reuse the stored proof's speculative copy (only the edges written).
+#ifndef QLZX_ENC_BAIL_SPEC
+#define QLZX_ENC_BAIL_SPEC 1
+#endif
+// Radix scatter: 64-element batches per iteration whose list loads are in flight together (the
+// second pass; the first reads no list).
+#ifndef QLZX_ENC_SCATTER_U
+#define QLZX_ENC_SCATTER_U 4
+#endif
+// Best match: sorted entries staged in LDS for this many consecutive 64-entry steps of a wave per
+// global-load wait (1 = one step per wait, the steps of a wave T entries apart).
+#ifndef QLZX_ENC_MATCH_STAGE
+#define QLZX_ENC_MATCH_STAGE 4
+#endif
 // Bucket starts of the 64 KiB kernel in LDS (8 KiB) rather than in the workgroup's global slot.
 #ifndef QLZX_ENC_BST_LDS
 #define QLZX_ENC_BST_LDS 1
@@ -236,7 +250,7 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
     const uint32_t per = (P + 64 * W - 1) / (64 * W) * 64;
     const uint32_t r0 = min(P, wave * per), r1 = min(P, r0 + per);
     const uint32_t per_magic = 0xFFFFFFFFu / per + 1u;  // umulhi(x, per_magic) = x / per for x < 2^16
-    constexpr uint32_t U = 4;  // 64-element batches per iteration: their list loads are in flight together
+    constexpr uint32_t U = sizeof(OUT) == 4 ? QLZX_ENC_SCATTER_U : 4;  // 64-element batches per iteration
     SUB_MARK(0);
     if (!counted) {
         for (uint32_t k = tid; k < cslots(NB, W); k += T) cnt[k] = 0;
@@ -313,7 +327,11 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
         // every lane's read is issued before the leader's write (in-order LDS per wave)
         if (valid && intra == 0) cnt[cslot<W>(key * W + wave)] = cur + (uint32_t)__popcll(peers);
         if (valid) {
+#ifdef QLZX_EXP_SCATTER_LINEAR  // timing experiment only (wrong output): stores in input order
+            out[sizeof(OUT) == 4 ? j : cur + intra] = (OUT)(sizeof(OUT) == 2 ? p : p | ((f >> 12) << 16));
+#else
             out[cur + intra] = (OUT)(sizeof(OUT) == 2 ? p : p | ((f >> 12) << 16));
+#endif
             if (next_cnt) atomicAdd(&next_cnt[cslot<W>((h >> 4) * W + __umulhi(cur + intra, per_magic))], 1u);
         }
       }
@@ -444,6 +462,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
         bool stored = false;
         bool prefix = false;  // try the prefix-only pass first (below, phase 4)
         bool cmode = false;   // compact best-match loop (phase 2)
+        bool spec = false;    // the proof wrote the stored value's aligned 16-B chunks
 
         PROF_MARK(0);  // 0: ticket + setup
         QLZX_TID_REFRESH();
@@ -499,7 +518,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             // value (header + input: chunk o holds input bytes o - 9 ..) go out now, each from the
             // window of the step 16 bytes before it.  A block that is not stored overwrites them
             // (its output is shorter; dst capacity is >= n + 400).
-            const bool spec = QLZX_ENC_SPEC_COPY && hdr == 9 && (((uintptr_t)dst) & 15u) == 0;
+            spec = QLZX_ENC_SPEC_COPY && hdr == 9 && (((uintptr_t)dst) & 15u) == 0;
             const uint32_t sa1 = (n + hdr) & ~15u;
             auto spec16 = [&](uint32_t y0, const uint32_t w[6]) {
                 if (spec && y0 + 32 <= sa1)
@@ -618,17 +637,36 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 // memory once per wave-iteration into an 80-word LDS stage (s_scr is free between
                 // the sort and the parse) and the 16 candidate reads per position are LDS reads
                 // of consecutive words, not 16 global loads.
-                static_assert(C::SCR >= 80 * W, "candidate stage");
-                uint32_t *stg = s_scr + wave * 80;
+                // With QLZX_ENC_MATCH_STAGE = S > 1 a wave takes S consecutive steps (64 S entries)
+                // at a time: their S + 1 list loads are issued together and waited for once.
+                constexpr uint32_t S = QLZX_ENC_MATCH_STAGE, SW = 64 * S + 16;
+                static_assert(C::SCR >= SW * W, "candidate stage");
+                uint32_t *const stg0 = s_scr + wave * SW;
                 auto best_matches = [&](auto compact) {
-                  for (uint32_t t0 = tid - lane; t0 < P; t0 += T) {  // wave-uniform
+                  for (uint32_t tb = (tid - lane) * S; tb < P; tb += T * S) {  // wave-uniform
+                    if (S > 1) {
+                        uint32_t v[S];
+#pragma unroll
+                        for (uint32_t u = 0; u < S; u++) v[u] = tb + 64 * u + lane < P ? gl[tb + 64 * u + lane] : 0u;
+                        const uint32_t halo = (lane < 16 && tb + lane >= 16) ? gl[tb + lane - 16] : 0u;
+#pragma unroll
+                        for (uint32_t u = 0; u < S; u++) stg0[16 + 64 * u + lane] = v[u];
+                        if (lane < 16) stg0[lane] = halo;
+                    }
+                  for (uint32_t u = 0; u < S; u++) {  // wave-uniform
+                    const uint32_t t0 = tb + 64 * u;
+                    if (t0 >= P) break;
+                    uint32_t *const stg = stg0 + 64 * u;
                     const uint32_t t = t0 + lane;
                     const bool act = t < P;
-                    const uint32_t self = act ? gl[t] : 0u;
-                    const uint32_t halo = (lane < 16 && t0 + lane >= 16) ? gl[t0 + lane - 16] : 0u;
-                    stg[16 + lane] = self;
-                    if (lane < 16) stg[lane] = halo;
+                    if (S == 1) {
+                        const uint32_t self = act ? gl[t] : 0u;
+                        const uint32_t halo = (lane < 16 && t0 + lane >= 16) ? gl[t0 + lane - 16] : 0u;
+                        stg[16 + lane] = self;
+                        if (lane < 16) stg[lane] = halo;
+                    }
                     if (!act) continue;
+                    const uint32_t self = stg[16 + lane];
                     const uint32_t p = self & 0xFFFFu, fh = self >> 16;
                     const uint32_t rm = (t - (uint32_t)bst[hash12(fetch24(s_in, p))]) & 255u;
                     const uint32_t d = rm < 16u ? rm : 16u;
@@ -701,6 +739,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     }
                     s_l8[p] = (uint8_t)best;  // 0 = literal, else 3..255
                     if (best) goff[p] = (uint16_t)(p - bpos);
+                  }
                   }
                 };
                 if (cmode) best_matches(std::true_type{});
@@ -879,7 +918,9 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 QLZX_TID_REFRESH();
                 if ((((uintptr_t)dst) & 15u) == 0) {  // 16-B stores from the LDS copy of the input
                     const uint32_t tot = n + hdr, a0 = (hdr + 15u) & ~15u, a1 = tot & ~15u;
-                    for (uint32_t o = a0 + tid * 16; o < a1; o += T * 16) {
+                    // a bail-out emits nothing before this point, so after a speculative copy
+                    // only the edges are missing
+                    for (uint32_t o = a0 + tid * 16; o < (spec && QLZX_ENC_BAIL_SPEC ? a0 : a1); o += T * 16) {
                         const uint32_t q = o - hdr;
                         *(uint4 *)(dst + o) = make_uint4(ld32u(s_in, q), ld32u(s_in, q + 4), ld32u(s_in, q + 8),
                                                          ld32u(s_in, q + 12));

@@ -40,9 +40,9 @@ def blocks(kind):
 
 ws = batch.Workspace(dev)
 prof = torch.zeros(40, dtype=torch.int64, device=dev)
-for kind in ("random", "noisy", "text", "zeros"):
+for kind in os.environ.get("KINDS", "random,noisy,text,zeros").split(","):
     src = blocks(kind)
-    dst = batch.BlockBatch.empty_for([bs] * n, device=dev, pad=400)
+    dst = batch.BlockBatch.empty_for([bs] * n, device=dev, pad=int(os.environ.get("PAD", "400")))
     st0 = torch.full((n,), -1, dtype=torch.int32, device=dev)
     batch.compress(src, dst, crc_state=st0, max_len=bs, workspace=ws)
     torch.cuda.synchronize()

@@ -30,6 +30,14 @@ def blocks(kind):
 
 
 ws = batch.Workspace(dev)
+if os.environ.get("ENC_ONE"):  # tools/enc_one.py: one class, REPS calls, no timing
+    src = blocks(os.environ["ENC_ONE"])
+    dst = batch.BlockBatch.empty_for([bs] * n, device=dev, pad=400)
+    st0 = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    for _ in range(int(os.environ.get("REPS", "2"))):
+        batch.compress(src, dst, crc_state=st0, max_len=bs, workspace=ws)
+    torch.cuda.synchronize()
+    sys.exit(0)
 for kind in ("random", "image", "noisy", "text", "zeros"):
     src = blocks(kind)
     dst = batch.BlockBatch.empty_for([bs] * n, device=dev, pad=400)
