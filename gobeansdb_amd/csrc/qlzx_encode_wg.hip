@@ -202,7 +202,14 @@ constexpr uint32_t kMatchCompactMax = QLZX_ENC_MATCH_COMPACT;
 #ifndef QLZX_ENC_BST_LDS
 #define QLZX_ENC_BST_LDS 1
 #endif
-constexpr uint32_t kPrefixMinLen = QLZX_ENC_PREFIX ? 16384 : 0xFFFFFFFFu, kPrefixRepeatPct = 28, kPrefixMargin = 1024;
+#ifndef QLZX_ENC_PREFIX_PCT
+#define QLZX_ENC_PREFIX_PCT 28
+#endif
+#ifndef QLZX_ENC_PREFIX_MARGIN
+#define QLZX_ENC_PREFIX_MARGIN 1024
+#endif
+constexpr uint32_t kPrefixMinLen = QLZX_ENC_PREFIX ? 16384 : 0xFFFFFFFFu, kPrefixRepeatPct = QLZX_ENC_PREFIX_PCT,
+                   kPrefixMargin = QLZX_ENC_PREFIX_MARGIN;
 constexpr uint32_t kParseRounds = 4;  // segment-walker rounds before the serial item walk
 
 // One pass of a stable LSD radix partition of the searched positions by
