@@ -103,3 +103,28 @@ def test_go_api_level1_round_trip(cuda, l1):
     del bad[40:]
     with pytest.raises(Q.QuicklzError):
         Q.Decompress(bytes(bad))
+
+
+def test_go_l1_batches_past_one_launch(cuda):
+    """More blocks than one level-1 launch takes (kL1Chunk = 65536, qlzx_api.hip): the chunks
+    reuse one workspace with chunk-local indices.  Every block in both chunks equals the oracle
+    byte for byte and decodes back through go_decompress."""
+    import torch
+    from gobeansdb_amd import batch
+    rng = random.Random(5)
+    words = [b"alpha ", b"beta ", b"gamma ", b"delta ", b"value:", b"0123", b"\x00\x01", b"key_"]
+    datas = []
+    for i in range(65536 + 37):
+        n = rng.randrange(1, 160)
+        d = b"".join(rng.choice(words) for _ in range(n // 4 + 1))[:n]
+        datas.append(d)
+    src = batch.BlockBatch.from_bytes(datas)
+    dst, cs, st = batch.go_l1_compress(src)
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().tolist() == [0] * len(datas)
+    outs = dst.to_bytes(cs.cpu().numpy())
+    for i, (d, o) in enumerate(zip(datas, outs)):
+        assert o == O.compress_go_l1(d), i
+    st2, back = _decode_batch(outs, [len(d) for d in datas])
+    assert st2 == [0] * len(datas)
+    assert back == datas
