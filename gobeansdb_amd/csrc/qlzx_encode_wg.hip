@@ -184,6 +184,10 @@ constexpr uint32_t kEncGroups = 256;  // bucket groups (hash >> 4), 16 buckets e
 #define QLZX_ENC_MATCH_COMPACT 10
 #endif
 constexpr uint32_t kMatchCompactMax = QLZX_ENC_MATCH_COMPACT;
+// Stored proof: 16-position steps per thread whose input loads are issued together.
+#ifndef QLZX_ENC_PROOF_STEPS
+#define QLZX_ENC_PROOF_STEPS 4
+#endif
 // Bail-out after a parse: reuse the stored proof's speculative copy (only the edges written).
 #ifndef QLZX_ENC_BAIL_SPEC
 #define QLZX_ENC_BAIL_SPEC 1
@@ -533,17 +537,23 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                         __builtin_amdgcn_alignbyte(w[2], w[1], 3), __builtin_amdgcn_alignbyte(w[3], w[2], 3),
                         __builtin_amdgcn_alignbyte(w[4], w[3], 3), __builtin_amdgcn_alignbyte(w[5], w[4], 3));
             };
-            // two 16-position steps per iteration, both loads in flight before either is hashed
-            for (uint32_t y0 = tid * 16; y0 < ny; y0 += 2 * T * 16) {
-                uint32_t wa[6] = {0, 0, 0, 0, 0, 0}, wb[6] = {0, 0, 0, 0, 0, 0};
-                const uint32_t y1 = y0 + T * 16;
-                load20(y0, wa);
-                if (y1 < ny) load20(y1, wb);
-                mark16(y0, wa);
-                spec16(y0, wa);
-                if (y1 < ny) {
-                    mark16(y1, wb);
-                    spec16(y1, wb);
+            // QLZX_ENC_PROOF_STEPS 16-position steps per iteration (4: a whole block of any class
+            // in one iteration), every load in flight before any step is hashed
+            constexpr uint32_t PS = QLZX_ENC_PROOF_STEPS;
+            for (uint32_t y0 = tid * 16; y0 < ny; y0 += PS * T * 16) {
+                uint32_t w[PS][6];
+#pragma unroll
+                for (uint32_t j = 0; j < PS; j++) {
+#pragma unroll
+                    for (uint32_t k = 0; k < 6; k++) w[j][k] = 0;
+                    if (y0 + j * T * 16 < ny) load20(y0 + j * T * 16, w[j]);
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < PS; j++) {
+                    if (y0 + j * T * 16 < ny) {
+                        mark16(y0 + j * T * 16, w[j]);
+                        spec16(y0 + j * T * 16, w[j]);
+                    }
                 }
             }
             __syncthreads();
