@@ -1013,14 +1013,19 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             //         ^ raw_{nst-1}
             // (a stripe's CRC shifted over the bytes after it; the state over all of them).
             if (wave == 0) {
-                uint32_t v = 0;
-                if (lane + 1 < nst) v = gf2_mulmod(g_crc_stripe[nst - 2 - lane], s_misc[4 + lane]);
-                else if (lane == 63) v = gf2_mulmod(g_crc_stripe[nst - 1], crc_state[i]);
+                // one GF(2) product per lane, operands selected (branches would run the lanes'
+                // products one after another): lanes < nst - 1 the stripes, 63 the state, 62
+                // x^(8L) for the last stripe's length L; then the one remaining product
+                const uint32_t last = csz - (nst - 1) * 4096;  // 1..4096
+                uint32_t a = 0, c = 0;
+                if (lane + 1 < nst) a = g_crc_stripe[nst - 2 - lane], c = s_misc[4 + lane];
+                if (lane == 63) a = g_crc_stripe[nst - 1], c = crc_state[i];
+                if (lane == 62) a = g_crc_piece[last >> 6], c = g_crc_byte[last & 63];
+                uint32_t v = gf2_mulmod(a, c);
+                const uint32_t xp = last == 4096 ? g_crc_pow[12] : __shfl(v, 62, 64);
+                if (lane == 62) v = 0;
                 for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
-                if (lane == 0) {
-                    const uint32_t last = csz - (nst - 1) * 4096;  // 1..4096
-                    crc_out[i] = ~(gf2_mulmod(crc_xpow_bytes(last), v) ^ s_misc[4 + nst - 1]);
-                }
+                if (lane == 0) crc_out[i] = ~(gf2_mulmod(xp, v) ^ s_misc[4 + nst - 1]);
             }
         }
         PROF_MARK(6);  // 6: CRC
