@@ -156,3 +156,42 @@ def test_wg_encoder_prefix_first_pass(cuda, n):
     outs = _check(blocks, max_len=65536)
     kinds = [o[0] & 1 for o in outs]  # header bit 0: compressed
     assert 0 < sum(kinds) < len(kinds), kinds  # both stored and compressed outcomes are covered
+
+
+def test_wg_encoder_unaligned_source_and_destination(cuda):
+    """Source and destination offsets off the 16-B grid.  An unaligned source skips the stored
+    proof (the block then runs the full parse); an unaligned destination turns off the proof's
+    speculative stored copy, so a bail-out after the parse must write the whole stored value
+    itself.  Every output equals the oracle and its fused CRC equals zlib's."""
+    import torch
+    from gobeansdb_amd import batch
+    rng = np.random.default_rng(31)
+    n = 65536
+    blocks = [_noisy(rng, O.gen_text(6, n, n), 0.42), rng.integers(0, 256, n, dtype=np.uint8).tobytes(),
+              O.gen_text(5, n, n), _noisy(rng, O.gen_text(8, 30000, 30000), 0.42), O.gen_image(9, n, n),
+              _noisy(rng, O.gen_text(10, n, n), 0.42)]
+    src_shift = [0, 5, 0, 3, 0, 0]
+    dst_shift = [3, 8, 1, 0, 12, 4]
+    so, do, tot_s, tot_d = [], [], 0, 0
+    for b, ss, ds in zip(blocks, src_shift, dst_shift):
+        so.append(tot_s + ss)
+        tot_s += ss + len(b) + 256
+        do.append(tot_d + ds)
+        tot_d += ds + len(b) + 400 + 256
+    host = np.zeros(tot_s, np.uint8)
+    for o, b in zip(so, blocks):
+        host[o:o + len(b)] = np.frombuffer(b, np.uint8)
+    lens = torch.tensor(np.asarray([len(b) for b in blocks], np.uint32).view(np.int32), device="cuda")
+    src = batch.BlockBatch(torch.from_numpy(host).cuda(), torch.tensor(so, dtype=torch.int64, device="cuda"), lens)
+    dst = batch.BlockBatch(torch.zeros(tot_d, dtype=torch.uint8, device="cuda"),
+                           torch.tensor(do, dtype=torch.int64, device="cuda"), lens.clone())
+    _, cs, st, crc = batch.compress(src, dst, want_crc=True, max_len=n)
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().tolist() == [0] * len(blocks)
+    outs = dst.to_bytes(cs.cpu().numpy())
+    crc = crc.cpu().numpy().view(np.uint32)
+    for i, (b, o) in enumerate(zip(blocks, outs)):
+        assert o == O.compress(b), i
+        assert int(crc[i]) == zlib.crc32(o), i
+    stored = [o[0] & 1 == 0 for o in outs]
+    assert stored[1] and not stored[2]  # the random block is stored, the text block is not
