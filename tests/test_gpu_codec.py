@@ -222,12 +222,13 @@ def test_record_fused_crc_verify(cuda, golden, general):
 
 @pytest.mark.parametrize("crc", [False, True])
 def test_multi_chunk_overlap_round_trip(cuda, crc):
-    """More blocks than one decode chunk (131072): K1 of chunk c+1 runs on the side stream while K2
-    of chunk c runs (two workspace halves).  Every block must round-trip, and with crc the fused
-    record CRC must equal a separate CRC pass over the compressed values."""
+    """More blocks than one decode chunk (262144 when max_dsize <= 16 KiB, chunk_blocks in
+    qlzx_decode_wave.hip): K1 of chunk c+1 runs on the side stream while K2 of chunk c runs (two
+    workspace halves).  Every block must round-trip, and with crc the fused record CRC must equal
+    a separate CRC pass over the compressed values."""
     import torch
     from gobeansdb_amd import batch
-    n = 131072 + 9000
+    n = 262144 + 9000
     lens = [256 + (i * 37) % 1800 for i in range(n)]
     plain = batch.synth("text", 77, lens)
     comp, cs, st, _ = batch.compress(plain, max_len=max(lens))
