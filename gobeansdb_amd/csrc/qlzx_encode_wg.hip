@@ -65,9 +65,26 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t *lds, uint32_t a) {
 __device__ __forceinline__ uint32_t fetch24(const uint8_t *lds, uint32_t p) { return ld32u(lds, p) & 0xFFFFFFu; }
 __device__ __forceinline__ uint32_t hash12(uint32_t f) { return ((f >> 12) ^ f) & (QLZX_BUCKETS - 1); }
 
+#ifndef QLZX_ENC_PEERS_BITOP
+#define QLZX_ENC_PEERS_BITOP 1
+#endif
 // Lanes (within `act`) whose NB-bit key equals this lane's key.
+// Per key bit: an all-ones / zero lane mask from one sign-extending bit extract, the ballot of
+// it, and m &= ~(B ^ mask) on each 32-bit half (one three-input bit op each; the select form
+// `set ? B : ~B` compiled to nine VALU ops per bit).
 template <int NB>
 __device__ __forceinline__ uint64_t match_peers(uint32_t key, uint64_t act) {
+#if QLZX_ENC_PEERS_BITOP
+    uint32_t lo = (uint32_t)act, hi = (uint32_t)(act >> 32);
+#pragma unroll
+    for (int bi = 0; bi < NB; bi++) {
+        const uint32_t sm = (uint32_t)((int32_t)(key << (31 - bi)) >> 31);  // all ones iff bit bi set
+        const uint64_t B = __ballot(sm != 0u);
+        lo &= ~((uint32_t)B ^ sm);
+        hi &= ~((uint32_t)(B >> 32) ^ sm);
+    }
+    return ((uint64_t)hi << 32) | lo;
+#else
     uint64_t m = act;
 #pragma unroll
     for (int bi = 0; bi < NB; bi++) {
@@ -76,6 +93,7 @@ __device__ __forceinline__ uint64_t match_peers(uint32_t key, uint64_t act) {
         m &= set ? B : ~B;
     }
     return m;
+#endif
 }
 
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t x, uint32_t d) {
