@@ -702,7 +702,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     }
                     if (!act) continue;
                     const uint32_t self = stg[16 + lane];
-                    const uint32_t p = self & 0xFFFFu, fh = self >> 16;
+                    const uint32_t p = self & 0xFFFFu;
                     const uint32_t rm = (t - (uint32_t)bst[hash12(fetch24(s_in, p))]) & 255u;
                     const uint32_t d = rm < 16u ? rm : 16u;
                     const uint32_t limit = min(255u, n - 4u - p);  // quicklz.c:310
@@ -722,15 +722,21 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                             bpos = q;
                         }
                     };
+                    // A candidate can match when it is in the bucket (k < d) with the same
+                    // fetch[23:12] (same bucket + same fetch[23:12] = same 3 bytes) and
+                    // o < src - MINOFFSET (q + 3 <= p): with fhs = fetch[23:12] << 16, the word
+                    // c - fhs is q when the fetch bits agree and >= 2^16 otherwise, so one
+                    // subtraction and one compare against p - 3 test both (no candidate at p < 3).
+                    const uint32_t fhs = self & 0xFFFF0000u, lim3 = p - 3u;
+                    const uint32_t dmask = p >= 3u ? (1u << d) - 1u : 0u;
                     if constexpr (decltype(compact)::value) {
-                        // candidates that can match: same bucket + same fetch[23:12] = same 3
-                        // bytes, o < src - MINOFFSET (stage words past d: masked)
                         uint32_t okm = 0;
 #pragma unroll
                         for (uint32_t k = 0; k < 16; k++) {
                             const uint32_t c = stg[15u + lane - k];
-                            okm |= (k < d && (c >> 16) == fh && (c & 0xFFFFu) + 3u <= p) ? 1u << k : 0u;
+                            okm |= (c - fhs <= lim3) ? 1u << k : 0u;
                         }
+                        okm &= dmask;
                         if (__ballot((uint32_t)__popc(okm) > kMatchCompactMax) == 0ull) {  // wave-uniform
                             for (uint32_t t2 = okm; t2; t2 &= t2 - 1u) {  // set bits, most recent first
                                 const uint32_t k = (uint32_t)__builtin_ctz(t2);
@@ -745,11 +751,8 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
 #pragma unroll
                         for (uint32_t k = 0; k < 16; k++) cand[k] = stg[k < d ? 15u + lane - k : 16u + lane];
 #pragma unroll
-                        for (uint32_t k = 0; k < 16; k++) {
-                            const uint32_t q = cand[k] & 0xFFFFu;
-                            // same bucket + same fetch[23:12] = same 3 bytes; o < src - MINOFFSET
-                            first(k, q, k < d && (cand[k] >> 16) == fh && q + 3u <= p);
-                        }
+                        for (uint32_t k = 0; k < 16; k++)
+                            first(k, cand[k] & 0xFFFFu, (((dmask >> k) & 1u) & (cand[k] - fhs <= lim3 ? 1u : 0u)) != 0u);
                     }
                     if (longm) best = 0;  // a long candidate always wins
                     while (longm && best < limit) {
