@@ -24,6 +24,9 @@
 #ifndef QLZX_K1_STRUCT
 #define QLZX_K1_STRUCT 0
 #endif
+#ifndef QLZX_K2_JUMP_BALLOTS  // pointer jumping's loop test from per-byte ballots
+#define QLZX_K2_JUMP_BALLOTS 1
+#endif
 #ifndef QLZX_K1_V4M2  // k_dec_parse4 takes a second match from the same dword, as k_dec_parse does
 #define QLZX_K1_V4M2 1
 #endif
@@ -588,6 +591,19 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
                     uint32_t t[B];
 #pragma unroll
                     for (uint32_t j = 0; j < B; j++) t[j] = spb[(qa[j] ? sv[j] : p0 + j) - c];
+#if QLZX_K2_JUMP_BALLOTS
+                    // the wave's "any byte still jumping" as an OR of per-byte ballots (scalar
+                    // masks), not an OR of the lanes' bools (packed into a bit vector per lane)
+                    uint64_t anym = 0;
+#pragma unroll
+                    for (uint32_t j = 0; j < B; j++) {
+                        // a byte whose source's source is outside the chunk or a literal is final
+                        qa[j] = t[j] - c < sv[j] - c;
+                        anym |= __ballot(qa[j]);
+                        sv[j] = t[j];
+                    }
+                    anyq = anym != 0;
+#else
                     anyq = false;
 #pragma unroll
                     for (uint32_t j = 0; j < B; j++) {
@@ -596,13 +612,18 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
                         anyq = anyq || qa[j];
                         sv[j] = t[j];
                     }
+#endif
 #pragma unroll
                     for (uint32_t h = 0; h < B; h += 4)
                         *(uint4 *)(mkl + h) = make_uint4(sv[h], sv[h + 1], sv[h + 2], sv[h + 3]);
 #ifdef QLZX_PROFILE
                     _pacc[7] += 1;
 #endif
+#if QLZX_K2_JUMP_BALLOTS
+                } while (anyq);
+#else
                 } while (__ballot(anyq));
+#endif
             }
             PROF_MARK(2);
             uint32_t vb[B];
