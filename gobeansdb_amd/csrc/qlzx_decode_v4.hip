@@ -24,6 +24,9 @@
 #ifndef QLZX_K1_STRUCT
 #define QLZX_K1_STRUCT 0
 #endif
+#ifndef QLZX_K1_LANELOOP  // K1's step loop as a per-lane loop instead of a ballot-tested one
+#define QLZX_K1_LANELOOP 1
+#endif
 #ifndef QLZX_K2_JUMP_BALLOTS  // pointer jumping's loop test from per-byte ballots
 #define QLZX_K2_JUMP_BALLOTS 1
 #endif
@@ -134,7 +137,11 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
             }
 #else
         bool go = true;
+#if QLZX_K1_LANELOOP
+        while (go) {  // per-lane loop: the exec mask carries go (no cross-lane op in the step)
+#else
         while (__ballot(go)) {
+#endif
 #ifdef QLZX_PROFILE
             _pacc[5] += 1;
             if (go) _pacc[6] += 1;
