@@ -262,9 +262,13 @@ def main():
         # PMC-measured HBM bytes per block (tools/traffic.py) x blocks per launch: a committed
         # measurement of this workload (FETCH_SIZE x 2 + WRITE_SIZE passes), not a counter of this run
         tj = json.load(open(args.traffic_json))
-        traffic = round(tj["hbm_bytes_per_block"] * n)
-        traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: {tj['hbm_bytes_per_block']:.0f} B/block "
-                       f"(PMC, committed) x {n} blocks")
+        per_block = tj.get("hbm_bytes_per_block")
+        if per_block is None and tj.get("hbm_bytes_per_call") and tj.get("nblocks_per_call"):
+            per_block = tj["hbm_bytes_per_call"] / tj["nblocks_per_call"]
+        if per_block is not None:  # an unreadable profile leaves traffic null rather than no line
+            traffic = round(per_block * n)
+            traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: {per_block:.0f} B/block "
+                           f"(PMC, committed) x {n} blocks")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N = 1 only
@@ -477,9 +481,10 @@ def bench_compress(args, rank, world, dev, kind, emit: bool = True):
     traffic_src = None
     tj = args.traffic_json or os.path.join(ROOT, "profiles", "r04_c3_traffic.json")
     if os.path.exists(tj) and kind == "image" and bs == 65536:
-        tpb = json.load(open(tj))["hbm_bytes_per_block"]
-        traffic = round(tpb * n)
-        traffic_src = f"{os.path.relpath(tj, ROOT)}: {tpb:.0f} B/block (PMC, committed) x {n} blocks"
+        tpb = json.load(open(tj)).get("hbm_bytes_per_block")
+        if tpb is not None:
+            traffic = round(tpb * n)
+            traffic_src = f"{os.path.relpath(tj, ROOT)}: {tpb:.0f} B/block (PMC, committed) x {n} blocks"
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N = 1 only
         ns = min(256, n)
