@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -13,12 +14,31 @@ OUT = os.path.join(HERE, "libqlzx.so")
 ARCH = os.environ.get("QLZX_ARCH", "gfx950")
 
 
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) of every csrc/* file and include/qlzx.h, by name and content:
+    compiled into the library (qlzx_info: "src <hash>"), so a binary is tied to the sources."""
+    h = hashlib.sha256()
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*"))) + [os.path.join(ROOT, "include", "qlzx.h")]
+    for s in srcs:
+        if os.path.isfile(s):
+            h.update(os.path.relpath(s, ROOT).encode() + b"\0")
+            with open(s, "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def embedded_hash(path: str = OUT) -> str | None:
+    """The source hash compiled into a built library (None if absent)."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        data = f.read()
+    i = data.find(b"qlzx-src-hash:")
+    return data[i + 14:i + 30].decode() if i >= 0 else None
+
+
 def _stale() -> bool:
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    srcs = glob.glob(os.path.join(CSRC, "*")) + [os.path.join(ROOT, "include", "qlzx.h")]
-    return any(os.path.getmtime(s) > t for s in srcs)
+    return embedded_hash(OUT) != source_hash()
 
 
 PROF_OUT = os.path.join(HERE, "libqlzx_prof.so")
@@ -26,7 +46,7 @@ PROF_OUT = os.path.join(HERE, "libqlzx_prof.so")
 
 def _compile(out: str, extra: list[str], verbose: bool) -> None:
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-Wno-unused-parameter", *extra,
+           "-Wall", "-Wno-unused-function", "-Wno-unused-parameter", f"-DQLZX_SRC_HASH=\"{source_hash()}\"", *extra,
            "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp",
            os.path.join(CSRC, "qlzx_api.hip")]
     if verbose:

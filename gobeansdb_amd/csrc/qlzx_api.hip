@@ -68,12 +68,18 @@ extern "C" {
 
 const char *qlzx_last_error(void) { return t_last_error.c_str(); }
 
+#ifndef QLZX_SRC_HASH
+#define QLZX_SRC_HASH "unknown"
+#endif
+// the source hash of the build (gobeansdb_amd/build.py source_hash); also greppable in the binary
+extern __attribute__((used)) const char qlzx_src_hash_tag[] = "qlzx-src-hash:" QLZX_SRC_HASH;
+
 int qlzx_info(char *buf, size_t len) {
     const char *s =
         "libqlzx: QuickLZ 1.4.1 level 3 + record CRC32 for gobeansdb; target gfx950 (MI355X); "
         "decode: wave-per-block LDS history (dsize<=" QLZX_STR(QLZX_FAST_MAX_DSIZE)
         ") + lane-per-block general; encode: workgroup-per-block position-parallel "
-        "(len<=" QLZX_STR(QLZX_WG_MAX_LEN) ") + lane-per-block general";
+        "(len<=" QLZX_STR(QLZX_WG_MAX_LEN) ") + lane-per-block general; src " QLZX_SRC_HASH;
     if (!buf || !len) return (int)strlen(s);
     snprintf(buf, len, "%s", s);
     return 0;

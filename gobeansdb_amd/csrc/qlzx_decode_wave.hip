@@ -424,6 +424,10 @@ constexpr uint32_t kWinB = QLZX_K2B_WIN, kMarkRing = QLZX_K2B_MR;
 #include "qlzx_decode_solo.hip"
 #include "qlzx_decode_small.hip"
 #include "qlzx_decode_v4.hip"
+#include "qlzx_decode_v5.hip"
+#ifndef QLZX_DEC_V5  // round-5 pair (k_dec_parse5 + k_dec_chunk5)
+#define QLZX_DEC_V5 0
+#endif
 #ifndef QLZX_DEC_V4
 #define QLZX_DEC_V4 1
 #endif
@@ -459,7 +463,10 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     const bool sort = chunk > 64;
     // two workspace halves when the caller gave room for them: K1 of chunk c+1 runs on a
     // side stream while K2 of chunk c runs on `s` (K1 is latency-bound at low occupancy)
-    const bool overlap = ws_bytes >= 2 * one && b.n > chunk0;
+#ifndef QLZX_OVERLAP  // 0: K1 and K2 of all chunks on the caller's stream, one after another (timing)
+#define QLZX_OVERLAP 1
+#endif
+    const bool overlap = QLZX_OVERLAP && ws_bytes >= 2 * one && b.n > chunk0;
     // per host thread (the batch API is re-entrant like the reference) and per device: the
     // side stream and events are created on the device that owns `s`
     struct Side {  // destroyed with the thread (Go runs cgo calls on many OS threads)
@@ -525,13 +532,19 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
         hipStream_t s1 = overlap ? side : s;
         if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
-        hipLaunchKernelGGL(QLZX_K1_GLOBAL ? k_dec_parse_g : ((QLZX_DEC_V4 && !QLZX_K1_V3) ? k_dec_parse4 : k_dec_parse),
+        hipLaunchKernelGGL(QLZX_DEC_V5 ? k_dec_parse5 : QLZX_K1_GLOBAL ? k_dec_parse_g : ((QLZX_DEC_V4 && !QLZX_K1_V3) ? k_dec_parse4 : k_dec_parse),
                            dim3((cnt + kParseWG - 1) / kParseWG),
                            dim3(kParseWG), 0, s1, b, dst_cap, dsize, status, first, cnt, info, recs, gmax, order,
                            max_dsize);
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
         // one kernel for every block size: the LDS window slides over longer blocks
-        if (QLZX_DEC_V4 && crc)
+        if (QLZX_DEC_V5 && crc)
+            hipLaunchKernelGGL(k_dec_chunk5<true>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
+                               recs, gmax, (const uint32_t *)order, crc_state, crc_expect, crc_out);
+        else if (QLZX_DEC_V5)
+            hipLaunchKernelGGL(k_dec_chunk5<false>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
+                               recs, gmax, (const uint32_t *)order, nullptr, nullptr, nullptr);
+        else if (QLZX_DEC_V4 && crc)
             hipLaunchKernelGGL(k_dec_chunk4<true>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
                                recs, gmax, (const uint32_t *)order, crc_state, crc_expect, crc_out);
         else if (QLZX_DEC_V4)

@@ -45,6 +45,15 @@ def test_info_names_gfx950():
     assert "gfx950" in _lib.info()
 
 
+def test_library_built_from_this_tree():
+    """The shipped libqlzx.so carries the hash of the sources it was compiled from
+    (build.source_hash over csrc/* + include/qlzx.h), and it is this tree's."""
+    _lib.lib()
+    h = build.source_hash()
+    assert build.embedded_hash() == h
+    assert ("src " + h) in _lib.info()
+
+
 def test_drop_ins_fail_stop_without_a_device():
     """The quicklz.h drop-ins have no error channel in their Go callers
     (quicklz/cquicklz.go:38-40, store/crc32.go:81-84): on a host with no GPU, qlz_compress,
