@@ -397,15 +397,19 @@ __device__ __forceinline__ void dec_v5r_block(K5rLds &L, const uint8_t *src, uin
         Wd = g_ld64(src + pa);
         mm |= (pos0 - pa) << 8;
     };
-    uint32_t pos0A, mmA, pos0B = 0, mmB = 0;
-    uint64_t WA, WB = 0;
+    // two batches in flight: at batch b the tokens of b + 1 and b + 2 and the GroupRecs of b + 3
+    // and b + 4 are loading (register sets A/B alternate between even and odd batches)
+    uint32_t pos0A, mmA, pos0B, mmB;
+    uint64_t WA, WB;
     GroupRec grA, grB;
     {
-        const GroupRec g0 = rb[min(gl, glast)];
+        const GroupRec g0 = rb[min(gl, glast)], g1 = rb[min(4 + gl, glast)];
         tok_fetch(g0, pos0A, mmA, WA);
-        grB = rb[min(4 + gl, glast)];
-        grA = grB;
+        tok_fetch(g1, pos0B, mmB, WB);
+        grA = rb[min(8 + gl, glast)];
+        grB = rb[min(12 + gl, glast)];
     }
+    uint32_t touch = 0;  // far sources touched ahead (into L2); consumed at the end of the block
     uint32_t D = 0, bt = 0, c = 0, cin = 0;
     bool tail = false, complete = false, err = false;
     bool pp0 = false, pp1 = false, anyp = false;
@@ -424,14 +428,15 @@ __device__ __forceinline__ void dec_v5r_block(K5rLds &L, const uint8_t *src, uin
         anyp = __ballot(pp0 || pp1) != 0;
     };
 
-    auto batch = [&](uint32_t pos0, uint32_t mm, uint64_t Wd, const GroupRec &gr_next, uint32_t &pos0_n,
-                     uint32_t &mm_n, uint64_t &W_n, GroupRec &gr_nn) __attribute__((always_inline)) {
+    auto batch = [&](uint32_t &pos0r, uint32_t &mmr, uint64_t &Wr, GroupRec &gr) __attribute__((always_inline)) {
         if (anyp) flush_pend();
         const uint32_t g = 4 * bt + gl;
         const uint32_t i0 = 31 * g + k0;
         const bool v0 = i0 < nitems, v1 = i0 + 1 < nitems && k0 < 30;
-        tok_fetch(gr_next, pos0_n, mm_n, W_n);
-        gr_nn = rb[min(4 * bt + 8 + gl, glast)];
+        const uint32_t pos0 = pos0r, mm = mmr;
+        uint64_t Wd = Wr;
+        tok_fetch(gr, pos0r, mmr, Wr);          // tokens of batch bt + 2
+        gr = rb[min(4 * bt + 16 + gl, glast)];  // GroupRecs of batch bt + 4
         Wd >>= 8 * (mm >> 8);
         const bool ism0 = v0 && (mm & 1u), ism1 = v1 && (mm & 2u);
         const uint32_t t0 = (uint32_t)Wd;
@@ -472,6 +477,13 @@ __device__ __forceinline__ void dec_v5r_block(K5rLds &L, const uint8_t *src, uin
         complete = __ballot(last) != 0;
         const uint32_t key0 = (d0 << 16) | (ism0 ? off0 : 0u);
         const uint32_t key1 = (d1 << 16) | (ism1 ? off1 : 0u);
+        {
+            // a match whose source will be older than the ring window: touch it now, so the chunk
+            // phase's far load hits L2 (unconditional loads: a conditional one would be waited on)
+            const bool f0 = live0 && ism0 && off0 + 2 * CH > W, f1 = live1 && ism1 && off1 + 2 * CH > W;
+            touch ^= *(g_u8 *)(dst + (f0 ? d0 - off0 : 0u));
+            touch ^= *(g_u8 *)(dst + (f1 ? d1 - off1 : 0u));
+        }
         const bool wr0 = live0 && d0 < c + MR, wr1 = live1 && d1 < c + MR;
         // a literal's byte goes to its own slot; a match's own slot holds a byte older than the valid
         // window (d < c + MR), so its token byte may go there too
@@ -588,12 +600,13 @@ __device__ __forceinline__ void dec_v5r_block(K5rLds &L, const uint8_t *src, uin
 
     for (;;) {
         if (bt >= nbt) { err = true; break; }  // stream ended before dsize (check C5)
-        batch(pos0A, mmA, WA, grB, pos0B, mmB, WB, grA);
+        batch(pos0A, mmA, WA, grA);
         if (err || chunks()) break;
         if (bt >= nbt) { err = true; break; }
-        batch(pos0B, mmB, WB, grA, pos0A, mmA, WA, grB);
+        batch(pos0B, mmB, WB, grB);
         if (err || chunks()) break;
     }
+    asm volatile("" ::"v"(touch));
     vm_sync();
     PROF_FLUSH(1);
     if (lane == 0) {
