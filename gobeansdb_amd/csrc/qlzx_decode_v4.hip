@@ -1,4 +1,4 @@
-// qlzx_decode_v4.hip -- round-4 batch decoder pair (dsize <= QLZX_FAST_MAX_DSIZE):
+// qlzx_decode_v4.hip -- the batch decoder pair (dsize <= QLZX_FAST_MAX_DSIZE), round 4:
 //
 // K1 k_dec_parse4  one LANE per block: the serial control-word chain of quicklz.c:513-671,
 //     one item STEP at a time (a literal run and the match that ends it, or a control word),
@@ -21,21 +21,6 @@
 //     token dword, so no prefetched register is copied (and waited for) at a batch boundary.
 //
 // Checks C1-C5 are applied exactly as by the oracle (oracle/qlz_oracle.c:180-231).
-#ifndef QLZX_K1_STRUCT
-#define QLZX_K1_STRUCT 0
-#endif
-#ifndef QLZX_K1_LANELOOP  // K1's step loop as a per-lane loop instead of a ballot-tested one
-#define QLZX_K1_LANELOOP 1
-#endif
-#ifndef QLZX_K2_JUMP_BALLOTS  // pointer jumping's loop test from per-byte ballots
-#define QLZX_K2_JUMP_BALLOTS 1
-#endif
-#ifndef QLZX_K1_V4M2  // k_dec_parse4 takes a second match from the same dword, as k_dec_parse does
-#define QLZX_K1_V4M2 1
-#endif
-#ifndef QLZX_K1_V4M3  // ... or up to three matches from an 8-byte window
-#define QLZX_K1_V4M3 0
-#endif
 namespace qlzx {
 
 // ------------------------------------------------------------------------------- K1 ----
@@ -86,66 +71,14 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
     for (uint32_t r = 0;; r++) {
         if (__ballot(stream && r <= last_round) == 0) break;
         PROF_MARK(0);
-#if QLZX_K1_ROUND == 64
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-#elif QLZX_K1_ROUND == 32
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-#else
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-#endif
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kPieces) : "memory");  // all but the newest two rounds
         PROF_MARK(1);
         const bool act = stream && r <= last_round;
         const uint32_t lim = (r + 1) * kRoundBytes - shift;  // stream bytes below lim have landed
         if (act && !done_parse) {
-#if QLZX_K1_STRUCT
-            // structured steps: a lane leaves the loop when its bytes run out (it resumes next
-            // round) or its stream ends; only active lanes update their state
-            for (;;) {
-#ifdef QLZX_PROFILE
-                _pacc[6] += 1;
-#endif
-                const bool gb = cwr == 1;
-                const uint32_t rem = csize - ip;
-                uint32_t run = __builtin_ctz(cwr);
-                run = run < rem ? run : rem;
-                const uint32_t q = ip + run;
-                const uint32_t rest = cwr >> run;
-                const bool hasm = (rest != 1u) & ((rest & 1u) != 0) & (q < csize);  // gb: rest == 1
-                if (ip + (gb ? 4u : 1u) > csize) { done_parse = true; break; }     // stream exhausted
-                if ((gb | hasm) && q + (gb ? 4u : 1u) > lim) break;                 // wait for the next round
-                const uint32_t w = ring_rd32(ring, q + shift, lane);
-                const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
-                const uint32_t e = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);  // token bytes - 1
-                if (gb) {
-                    if (((w >> 31) == 0) | (g >= gmax)) { st = QLZX_E_CORRUPT; done_parse = true; break; }  // C1
-                    if (g > 0) myrec[g - 1] = GroupRec{rec_ip, cwg, ra, rb};
-                    rec_ip = ip;
-                    cwg = w;
-                    cwr = w;
-                    ra = 0;
-                    rb = 0;
-                    ip += 4;
-                    g++;
-                } else {
-                    if (hasm & (q + e + 1 > csize)) { st = QLZX_E_CORRUPT; done_parse = true; break; }  // C2
-                    const uint32_t kb = hasm ? 1u << (__builtin_clz(cwr) + run) : 0u;
-                    ra |= (e & 1u) ? kb : 0u;
-                    rb |= (e & 2u) ? kb : 0u;
-                    ip = q + (hasm ? e + 1 : 0u);
-                    cwr = rest >> (hasm ? 1 : 0);
-                }
-            }
-#else
         bool go = true;
-#if QLZX_K1_LANELOOP
         while (go) {  // per-lane loop: the exec mask carries go (no cross-lane op in the step)
-#else
-        while (__ballot(go)) {
-#endif
-#ifdef QLZX_PROFILE
-            _pacc[5] += 1;
-            if (go) _pacc[6] += 1;
-#endif
+            PROF_COUNT(5, 1);
             const bool gb = cwr == 1;
             const uint32_t rem = csize - ip;
             uint32_t run = __builtin_ctz(cwr);  // literals before the next match (or the sentinel)
@@ -160,24 +93,6 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
             const uint32_t w = ring_rd32(ring, q + shift, lane);
             const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
             const uint32_t e = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);  // token bytes - 1
-#if QLZX_K1_V4M3
-            // up to three matches per step from an 8-byte window at q (the tokens' first bytes)
-            const uint32_t wh = ring_rd32(ring, q + 4 + shift, lane);
-            const uint64_t W8 = ((uint64_t)wh << 32) | w;
-            const uint32_t q2 = q + e + 1, rest2 = rest >> 1;
-            const bool hasm2 = hasm & ((rest2 & 1u) != 0) & (rest2 != 1u) & (q2 < csize) & (q2 + 1 <= lim);
-            const uint32_t t2 = (uint32_t)(W8 >> (8 * (e + 1)));
-            const uint32_t ty2 = (t2 & 3u) + ((t2 & 127u) == 3u ? 1u : 0u);
-            const uint32_t e2 = hasm2 ? __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4) : 0u;
-            const uint32_t q3 = q2 + e2 + 1, rest3 = rest2 >> 1;
-            const bool hasm3 = hasm2 & ((rest3 & 1u) != 0) & (rest3 != 1u) & (q3 < csize) & (q3 + 1 <= lim) &
-                               (e + e2 + 2 <= 7u);
-            const uint32_t t3 = (uint32_t)(W8 >> (8 * ((e + e2 + 2) & 7u)));
-            const uint32_t ty3 = (t3 & 3u) + ((t3 & 127u) == 3u ? 1u : 0u);
-            const uint32_t e3 = hasm3 ? __builtin_amdgcn_ubfe(0x32110u, ty3 * 4, 4) : 0u;
-            const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) | (hasm & (q2 > csize)) |
-                                         (hasm2 & (q3 > csize)) | (hasm3 & (q3 + e3 + 1 > csize)));
-#elif QLZX_K1_V4M2
             // a second match right after the first when its first byte is already in w
             const uint32_t q2 = q + e + 1, rest2 = rest >> 1;
             const bool hasm2 = hasm & (e < 3u) & ((rest2 & 1u) != 0) & (rest2 != 1u) & (q2 < csize) & (q2 + 1 <= lim);
@@ -186,31 +101,15 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
             const uint32_t e2 = hasm2 ? __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4) : 0u;
             const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) | (hasm & (q2 > csize)) |
                                          (hasm2 & (q2 + e2 + 1 > csize)));
-#else
-            const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) | (hasm & (q + e + 1 > csize)));
-#endif
             if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, cwg, ra, rb};
             st = bad ? QLZX_E_CORRUPT : st;
             const bool adv = stepping & !bad;
             const uint32_t kb = hasm ? 1u << (__builtin_clz(cwr) + run) : 0u;  // item index clz(cwr) + run
-#if QLZX_K1_V4M3
-            const uint32_t kb2 = hasm2 ? kb << 1 : 0u, kb3 = hasm3 ? kb << 2 : 0u;
-            const uint32_t nip = gb ? ip + 4 : q + (hasm ? e + 1 : 0u) + (hasm2 ? e2 + 1 : 0u) + (hasm3 ? e3 + 1 : 0u);
-            const uint32_t ncwr = gb ? w : (rest >> (hasm ? (hasm2 ? (hasm3 ? 3 : 2) : 1) : 0));
-            const uint32_t nra = gb ? 0u : (ra | ((e & 1u) ? kb : 0u) | ((e2 & 1u) ? kb2 : 0u) | ((e3 & 1u) ? kb3 : 0u));
-            const uint32_t nrb = gb ? 0u : (rb | ((e & 2u) ? kb : 0u) | ((e2 & 2u) ? kb2 : 0u) | ((e3 & 2u) ? kb3 : 0u));
-#elif QLZX_K1_V4M2
             const uint32_t kb2 = hasm2 ? kb << 1 : 0u;
             const uint32_t nip = gb ? ip + 4 : q + (hasm ? e + 1 : 0u) + (hasm2 ? e2 + 1 : 0u);
             const uint32_t ncwr = gb ? w : (rest >> (hasm ? (hasm2 ? 2 : 1) : 0));
             const uint32_t nra = gb ? 0u : (ra | ((e & 1u) ? kb : 0u) | ((e2 & 1u) ? kb2 : 0u));
             const uint32_t nrb = gb ? 0u : (rb | ((e & 2u) ? kb : 0u) | ((e2 & 2u) ? kb2 : 0u));
-#else
-            const uint32_t nip = gb ? ip + 4 : q + (hasm ? e + 1 : 0u);
-            const uint32_t ncwr = gb ? w : (rest >> (hasm ? 1 : 0));
-            const uint32_t nra = gb ? 0u : (ra | ((e & 1u) ? kb : 0u));
-            const uint32_t nrb = gb ? 0u : (rb | ((e & 2u) ? kb : 0u));
-#endif
             rec_ip = (adv & gb) ? ip : rec_ip;
             cwg = (adv & gb) ? w : cwg;
             g += (adv & gb) ? 1u : 0u;
@@ -221,7 +120,6 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
             done_parse = done_parse | (go & (end | bad));
             go = adv;
         }
-#endif
         }
         PROF_MARK(3);
         if (done_parse) stream = false;
@@ -248,135 +146,10 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
     info[lin] = bi;
 }
 
-// ------------------------------------------------------------- K1 without the LDS ring ----
-// k_dec_parse's step (a literal run and up to two matches, quicklz.c:513-671), reading each step's
-// dword straight from the stream in global memory (L1/L2; a lane's bytes are sequential) instead
-// of an LDS DMA ring: K1 then holds no LDS, so K2 of the previous chunk keeps its occupancy while
-// K1 runs beside it (the 16 KiB ring per K1 wave displaced three K2 waves each).
-__device__ __forceinline__ uint32_t g_rd32(const uint8_t *src, uint32_t q, uint32_t csize) {
-    const uint32_t qa = q + 4 <= csize ? q : csize - 4;  // csize >= 7 for a compressed stream
-    uint64_t a = (uint64_t)(uintptr_t)(src + qa);
-    asm volatile("" : "+v"(a));  // a vector load (any byte address), never a scalar one
-    return *(const uint32_t *)(uintptr_t)a >> (8 * (q - qa));
-}
-__global__ void __launch_bounds__(kParseWG) k_dec_parse_g(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
-                                                      int32_t *status, uint32_t first, uint32_t count, BlkInfo *info,
-                                                      GroupRec *recs, uint32_t gmax, const uint32_t *order,
-                                                      uint32_t max_dsize) {
-    const uint32_t lin = blockIdx.x * kParseWG + threadIdx.x;
-    const bool inrange = lin < count;
-    const uint32_t i = inrange ? (order ? order[lin] : first + lin) : first;
-    int st = QLZX_OK;
-    uint32_t kind = kBlkSkip, csize = 0, dsize = 0, hdr = 0;
-    const uint8_t *src = b.src + b.src_off[i];
-    if (inrange) {
-        st = classify_block(src, b.src_len[i], dst_cap ? dst_cap[i] : 0xffffffffu, max_dsize, kind, csize, dsize, hdr);
-        if (st == QLZX_OK && kind == kBlkCompressed && dsize == 0) {  // oracle/qlz_oracle.c:197,228
-            st = (csize == hdr || csize == hdr + 9) ? QLZX_OK : QLZX_E_CORRUPT;
-            kind = kBlkSkip;
-        }
-    }
-    const bool parsing = inrange && st == QLZX_OK && kind == kBlkCompressed;
-    uint32_t ip = hdr, g = 0, k = 31, cw = 0, m = 0, ra = 0, rb = 0, rec_ip = 0;
-    GroupRec *myrec = recs + (size_t)(inrange ? lin : 0) * gmax;
-    bool done_parse = !parsing, go = parsing;
-    PROF_DECL
-    while (__ballot(go)) {
-#ifdef QLZX_PROFILE
-        _pacc[5] += 1;
-        if (go) _pacc[6] += 1;
-#endif
-        const bool gb = k == 31;
-        const uint32_t kk = k & 31;
-        const uint32_t cwk = cw >> kk;
-        uint32_t run = __builtin_ctz(cwk | (1u << (31 - kk)));  // literals before the next match
-        run = gb ? 0u : (run < csize - ip ? run : csize - ip);
-        const uint32_t ipm = ip + run, km = kk + run;
-        const bool hasm = !gb & (km < 31) & (ipm < csize);
-        const bool end = ip + (gb ? 4u : 1u) > csize;
-        const bool stepping = go & !end & (gb | (run > 0) | hasm);
-        const uint32_t w = g_rd32(src, ipm, csize);
-        const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
-        const uint32_t code = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);
-        const uint32_t ip2 = ipm + code + 1, k2 = km + 1;
-        const uint32_t w2 = w >> (8 * ((code + 1) & 3));
-        const bool mat2 = hasm & (code < 3) & (k2 < 31) & (((cw >> (k2 & 31)) & 1u) != 0) & (ip2 < csize);
-        const uint32_t ty2 = (w2 & 3u) + ((w2 & 127u) == 3u ? 1u : 0u);
-        const uint32_t code2 = __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4);
-        bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) | (hasm & (ipm + code + 1 > csize)) |
-                               (mat2 & (ip2 + code2 + 1 > csize)));
-        if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
-        st = bad ? QLZX_E_CORRUPT : st;
-        const bool adv = stepping & !bad;
-        const bool ag = adv & gb;
-        const uint32_t bm = hasm ? (1u << (km & 31)) : 0u;
-        const uint32_t bm2 = mat2 ? (1u << (k2 & 31)) : 0u;
-        rec_ip = ag ? ip : rec_ip;
-        cw = ag ? w : cw;
-        g += ag ? 1u : 0u;
-        ip += adv ? (gb ? 4u : run + (hasm ? code + 1 : 0u) + (mat2 ? code2 + 1 : 0u)) : 0u;
-        k = adv ? (gb ? 0u : km + (hasm ? 1u : 0u) + (mat2 ? 1u : 0u)) : k;
-        m = adv ? (gb ? 0u : m | bm | bm2) : m;
-        ra = adv ? (gb ? 0u : ra | ((code & 1u) ? bm : 0u) | ((code2 & 1u) ? bm2 : 0u)) : ra;
-        rb = adv ? (gb ? 0u : rb | ((code & 2u) ? bm : 0u) | ((code2 & 2u) ? bm2 : 0u)) : rb;
-        done_parse = done_parse | (go & (end | bad | !stepping));
-        go = adv;
-    }
-    PROF_MARK(3);
-    if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
-    PROF_FLUSH(0);
-    vm_sync();
-    if (!inrange) return;
-    if (st == QLZX_OK && kind == kBlkCompressed && (!done_parse || g == 0)) st = QLZX_E_CORRUPT;
-    BlkInfo bi{0, 0, kind, dsize};
-    if (st != QLZX_OK) {
-        bi.kind = kBlkSkip;
-        status[i] = st;
-        if (dsize_out && st != kPending) dsize_out[i] = 0;
-    } else if (kind == kBlkCompressed) {
-        bi.ngroups = g;
-        bi.nitems = (g - 1) * 31 + (k > 31 ? 31 : k);
-    } else if (kind == kBlkSkip) {  // dsize-0 compressed stream accepted above
-        status[i] = QLZX_OK;
-        if (dsize_out) dsize_out[i] = 0;
-    }
-    info[lin] = bi;
-}
-
 // ------------------------------------------------------------------------------- K2 ----
-#ifndef QLZX_K2_BPL
-#define QLZX_K2_BPL 4
-#endif
-#ifndef QLZX_K2_ASM_STORE
-#define QLZX_K2_ASM_STORE 0
-#endif
-#ifndef QLZX_K2_COUNTED  // chunk loop with its trip count computed at entry
-#define QLZX_K2_COUNTED 0
-#endif
-#ifndef QLZX_K2_FARSEL  // literal window byte written for every item that marks (no nested branch)
-#define QLZX_K2_FARSEL 1
-#endif
-#ifndef QLZX_K2_FARALL  // far loads issued by every lane of a chunk with far bytes
-#define QLZX_K2_FARALL 0
-#endif
-#ifndef QLZX_K2_FARSPLIT
-#define QLZX_K2_FARSPLIT 0
-#endif
-#ifndef QLZX_K2_PRIO  // wave priority of K2 (s_setprio) over the overlapped K1
-#define QLZX_K2_PRIO 0
-#endif
-#ifndef QLZX_K2_EARLYFAR  // far loads issued before the pointer jumping: measured slower
-#define QLZX_K2_EARLYFAR 0
-#endif
-#ifndef QLZX_K2_WIN
-#define QLZX_K2_WIN 4096
-#endif
-#ifndef QLZX_K2_MR
-#define QLZX_K2_MR 256
-#endif
-constexpr uint32_t kV4W = QLZX_K2_WIN;   // output window (LDS ring)
-constexpr uint32_t kV4MR = QLZX_K2_MR;   // marker ring (u32 keys)
-constexpr uint32_t kV4Bpl = QLZX_K2_BPL;        // output bytes per lane per chunk (4 or 8)
+constexpr uint32_t kV4W = 4096;   // output window (LDS ring)
+constexpr uint32_t kV4MR = 256;   // marker ring (u32 keys)
+constexpr uint32_t kV4Bpl = 4;  // output bytes per lane per chunk
 constexpr uint32_t kV4Chunk = 64 * kV4Bpl;      // 256 or 512 output bytes per chunk
 static_assert(kV4Chunk <= kV4MR, "a chunk's pointer-jumping array lives in its marker slots");
 
@@ -506,13 +279,9 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
         const bool wr = live && d < c + MR;
         if (wr) {
             L.mk[d & (MR - 1)] = key;
-#if QLZX_K2_FARSEL
             // a match's own window slot holds a byte older than the far bound (d < c + MR) that no
             // gather reads before the chunk of d overwrites it: the byte can go there unconditionally
             L.win[d & (W - 1)] = (uint8_t)t;
-#else
-            if (!ism) L.win[d & (W - 1)] = (uint8_t)t;
-#endif
         }
         pend = __ballot(live && !wr);
         pd = d;
@@ -520,22 +289,12 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
         plit = ism ? 0x100u : (t & 0xffu);
         D = __builtin_amdgcn_readfirstlane(D + total);
         bt++;
-#ifdef QLZX_PROFILE
-        _pacc[5] += 1;
-#endif
+        PROF_COUNT(5, 1);
     };
 
     // chunk phases while every item starting below c + 256 is known; true when the block is done
     auto chunks = [&]() __attribute__((always_inline)) -> bool {
-#if QLZX_K2_COUNTED
-        // D does not move while chunks run: the number of ready chunks is known up front
-        const uint32_t left = c < dsize ? (dsize - c + CH - 1) / CH : 0u;
-        uint32_t nch = complete ? left : (D >= c + CH ? min((D - c) / CH, left) : 0u);
-        nch = __builtin_amdgcn_readfirstlane(nch);
-        for (; nch; nch--) {
-#else
         while (c < dsize && (complete || D >= c + CH)) {
-#endif
             if (pend) {  // items of the last batch that start at or above c_prev + MR
                 const bool wr = ((pend >> lane) & 1u) && pd < c + MR;
                 if (wr) {
@@ -570,25 +329,6 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
             }
             PROF_MARK(1);
             const uint32_t lo = c + MR > W ? c + MR - W : 0u;
-#if QLZX_K2_EARLYFAR
-            // bytes whose source is older than the window: their loads go out now and land while
-            // the pointer jumping and the window gather run (sources that jumping changes are in
-            // the chunk, so a byte is far here exactly when its final source is a direct far one)
-            uint32_t fv[B];
-            bool fd[B], anyfd = false;
-#pragma unroll
-            for (uint32_t j = 0; j < B; j++) {
-                fd[j] = sv[j] < lo;
-                anyfd = anyfd || fd[j];
-                fv[j] = 0;
-            }
-            const bool farq = __ballot(anyfd) != 0;
-            if (farq) {
-#pragma unroll
-                for (uint32_t j = 0; j < B; j++)
-                    if (fd[j]) fv[j] = dst[sv[j]];
-            }
-#endif
             if (__ballot(anyq)) {
                 // the chunk's marker slots are free once read: they hold each byte's current source
                 uint32_t *spb = L.mk + (c & (MR - 1));
@@ -598,7 +338,6 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
                     uint32_t t[B];
 #pragma unroll
                     for (uint32_t j = 0; j < B; j++) t[j] = spb[(qa[j] ? sv[j] : p0 + j) - c];
-#if QLZX_K2_JUMP_BALLOTS
                     // the wave's "any byte still jumping" as an OR of per-byte ballots (scalar
                     // masks), not an OR of the lanes' bools (packed into a bit vector per lane)
                     uint64_t anym = 0;
@@ -610,27 +349,11 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
                         sv[j] = t[j];
                     }
                     anyq = anym != 0;
-#else
-                    anyq = false;
-#pragma unroll
-                    for (uint32_t j = 0; j < B; j++) {
-                        // a byte whose source's source is outside the chunk or a literal is final
-                        qa[j] = t[j] - c < sv[j] - c;
-                        anyq = anyq || qa[j];
-                        sv[j] = t[j];
-                    }
-#endif
 #pragma unroll
                     for (uint32_t h = 0; h < B; h += 4)
                         *(uint4 *)(mkl + h) = make_uint4(sv[h], sv[h + 1], sv[h + 2], sv[h + 3]);
-#ifdef QLZX_PROFILE
-                    _pacc[7] += 1;
-#endif
-#if QLZX_K2_JUMP_BALLOTS
+                    PROF_COUNT(7, 1);
                 } while (anyq);
-#else
-                } while (__ballot(anyq));
-#endif
             }
             PROF_MARK(2);
             uint32_t vb[B];
@@ -638,93 +361,24 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
 #pragma unroll
             for (uint32_t j = 0; j < B; j++) {
                 vb[j] = L.win[sv[j] & (W - 1)];
-#if QLZX_K2_EARLYFAR
-                far = far || (sv[j] < lo && !fd[j]);  // reached a far source through the chunk
-#else
                 far = far || sv[j] < lo;
-#endif
             }
-#if QLZX_K2_EARLYFAR
-            if (farq) {
-#pragma unroll
-                for (uint32_t j = 0; j < B; j++) vb[j] = fd[j] ? fv[j] : vb[j];
-            }
-#endif
-#ifdef QLZX_PROFILE
-#if QLZX_K2_EARLYFAR
-            _pacc[6] += (__ballot(far) || farq) ? 1 : 0;  // chunks with a byte older than the window
-#else
-            _pacc[6] += __ballot(far) ? 1 : 0;  // chunks with a byte older than the window
-#endif
-#endif
+            PROF_COUNT(6, __ballot(far) ? 1 : 0);  // chunks with a byte older than the window
             uint32_t w[B / 4];
-#if QLZX_K2_FARSPLIT
-            // the far loads' wait stays inside their branch: a chunk without far bytes does not
-            // wait for the previous chunk's store and the prefetched loads at a merged vmcnt(0)
             if (__ballot(far)) {
 #pragma unroll
                 for (uint32_t j = 0; j < B; j++)
                     if (sv[j] < lo) vb[j] = dst[sv[j]];
-#pragma unroll
-                for (uint32_t h = 0; h < B / 4; h++) {
-                    w[h] = vb[4 * h] | (vb[4 * h + 1] << 8) | (vb[4 * h + 2] << 16) | (vb[4 * h + 3] << 24);
-                    asm volatile("" : "+v"(w[h]));
-                }
-            } else {
-#pragma unroll
-                for (uint32_t h = 0; h < B / 4; h++)
-                    w[h] = vb[4 * h] | (vb[4 * h + 1] << 8) | (vb[4 * h + 2] << 16) | (vb[4 * h + 3] << 24);
             }
-#else
-#ifndef QLZX_EXP_NOFAR  // (timing experiment: far bytes read from the window, wrong output)
-            if (__ballot(far)) {
-#if QLZX_K2_FARALL
-                // every lane loads (a lane without a far byte reads the block's first output byte, which
-                // it ignores): no exec-mask branch per byte -- measured slower (27.2 vs 27.0 ms on c2):
-                // the loads of lanes without far bytes cost more than the branches they save
-                uint32_t x[B];
-#pragma unroll
-                for (uint32_t j = 0; j < B; j++) x[j] = dst[sv[j] < lo ? sv[j] : 0u];
-                // one barrier over all loads keeps them out of per-byte branches and in flight together
-#pragma unroll
-                for (uint32_t h = 0; h < B; h += 4) asm volatile("" : "+v"(x[h]), "+v"(x[h + 1]), "+v"(x[h + 2]), "+v"(x[h + 3]));
-#pragma unroll
-                for (uint32_t j = 0; j < B; j++) vb[j] = sv[j] < lo ? x[j] : vb[j];
-#else
-#pragma unroll
-                for (uint32_t j = 0; j < B; j++)
-                    if (sv[j] < lo) vb[j] = dst[sv[j]];
-#endif
-            }
-#endif
 #pragma unroll
             for (uint32_t h = 0; h < B / 4; h++)
                 w[h] = vb[4 * h] | (vb[4 * h + 1] << 8) | (vb[4 * h + 2] << 16) | (vb[4 * h + 3] << 24);
-#endif
-            if constexpr (B == 8) {
-                *(uint2 *)(L.win + (p0 & (W - 1))) = make_uint2(w[0], w[1]);
-            } else {
-                *(uint32_t *)(L.win + (p0 & (W - 1))) = w[0];
-            }
+            *(uint32_t *)(L.win + (p0 & (W - 1))) = w[0];
 #pragma unroll
             for (uint32_t h = 0; h < B; h += 4) *(uint4 *)(mkl + h) = make_uint4(0, 0, 0, 0);  // slots of c + MR ..
             PROF_MARK(3);
             if (c + CH <= dsize) {
-#if QLZX_K2_ASM_STORE
-                // stored behind the compiler's back: with no store in its VM_CNT bookkeeping it waits
-                // for a prefetched load with vmcnt(N) instead of draining every store first (vm_sync()
-                // at the end of the block orders them before the status word)
-#pragma unroll
-                for (uint32_t h = 0; h < B / 4; h++)
-                    asm volatile("global_store_dword %0, %1, off" ::"v"(dst + p0 + 4 * h), "v"(w[h]) : "memory");
-#else
-                if constexpr (B == 8) {
-                    if ((((uintptr_t)dst) & 7u) == 0) *(uint2 *)(dst + p0) = make_uint2(w[0], w[1]);
-                    else *(uint32_t *)(dst + p0) = w[0], *(uint32_t *)(dst + p0 + 4) = w[1];
-                } else {
-                    *(uint32_t *)(dst + p0) = w[0];
-                }
-#endif
+                *(uint32_t *)(dst + p0) = w[0];
             } else {
                 for (uint32_t j = 0; j < B && p0 + j < dsize; j++) dst[p0 + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
             }
@@ -759,10 +413,6 @@ __global__ void __launch_bounds__(64) k_dec_chunk4(qlzx_blocks b, uint32_t *dsiz
                                                    const uint32_t *crc_state, const uint32_t *crc_expect,
                                                    uint32_t *crc_out) {
     __shared__ __attribute__((aligned(16))) K2v4Lds L;
-#if QLZX_K2_PRIO
-    // K2 waves first when they share a SIMD with the next chunk's K1 (which has slack)
-    __builtin_amdgcn_s_setprio(QLZX_K2_PRIO);
-#endif
     const uint32_t bx = blockIdx.x;
     if (bx >= count) return;
     const uint32_t i = list ? list[bx] : first + bx;

@@ -1,26 +1,12 @@
 // qlzx_decode_wave.hip -- fast batched level-3 decoder for blocks with
 // dsize <= QLZX_FAST_MAX_DSIZE (the 4-64 KiB values of the BASELINE configs).
 //
-// Kernels per chunk of blocks:
-//
-// K1 k_dec_parse  one LANE per block.  Walks the serial control-word/token
-//     chain of quicklz.c:513-671 once -- reading only control words and the
-//     first byte of each match token (its length) -- and emits one 16-B record
-//     per control-word group:
-//       ip  stream offset of the group's control word
-//       m   match mask (bit k = item k is a match)
-//       a,b bit-planes of (token bytes - 1) per match item (token length 1..4)
-//     Input arrives in rounds: every lane's next 64-B chunk is DMA'd
-//     (global_load_lds) into the same ring slot, one round ahead, so the M0
-//     base is wave-uniform and no register waits on in-flight loads.  A lane
-//     parses until it runs out of landed bytes, so rounds self-align by bytes.
-//
-// K2 k_dec_bytes (qlzx_decode_bytes.hip) one WAVE per block: when a record CRC
-//     is asked for it is verified first (store/datafile.go:161-168, the CRC of
-//     store/datafile.go:66-76 over the stored bytes; a mismatch is QLZX_E_CRC
-//     and nothing is written); then items are decoded 64 at a time, leaving one
-//     marker per item, and output is produced 256 bytes at a time, every byte
-//     gathered from the position it copies.
+// Kernels per chunk of blocks: K1 k_dec_parse4 (one LANE per block: the serial
+// control-word chain of quicklz.c:513-671, one 16-B GroupRec per control word) and K2
+// k_dec_chunk4 (one WAVE per block: items 64 at a time, output 256 bytes at a time, every byte
+// gathered from the position it copies; the record CRC is verified first when asked for,
+// store/datafile.go:161-168).  Both are in qlzx_decode_v4.hip; this file holds the shared
+// types, the block order, the header checks, K1's DMA ring and the launcher.
 //
 // K1 of chunk c+1 runs on a side stream beside K2 of chunk c.
 #include "qlzx_device.h"
@@ -64,16 +50,7 @@ __host__ __device__ inline uint32_t chunk_blocks(uint32_t max_dsize) {
 __host__ __device__ inline uint32_t first_chunk_blocks(uint32_t max_dsize) {
     return QLZX_FIRST_CHUNK < chunk_blocks(max_dsize) ? (uint32_t)QLZX_FIRST_CHUNK : chunk_blocks(max_dsize);
 }
-#ifndef QLZX_K1_NOMAT2  // K1 steps take one match at most (no second match from the same dword)
-#define QLZX_K1_NOMAT2 0
-#endif
-#ifndef QLZX_K1_MLATE  // a group's match bits taken from its control word when it is recorded
-#define QLZX_K1_MLATE 1
-#endif
-#ifndef QLZX_K1_ROUND  // bytes per lane per DMA round: 32 (8 KiB ring per wave) measured best with the v4 K2
-#define QLZX_K1_ROUND 32
-#endif
-constexpr uint32_t kRoundBytes = QLZX_K1_ROUND;  // bytes DMA'd per lane per round (16 B pieces)
+constexpr uint32_t kRoundBytes = 32;  // bytes DMA'd per lane per round (16 B pieces; 32 measured best)
 constexpr uint32_t kPieces = kRoundBytes / 16;
 constexpr uint32_t kRingSlots = 4;            // rounds resident per lane: r-1..r (read), r+1..r+2 (landing)
 constexpr uint32_t kRingWave = kRingSlots * kRoundBytes * 64;  // 16 KiB per wave at 64-B rounds
@@ -213,156 +190,7 @@ __device__ __forceinline__ void ring_issue(uint8_t *ring_wave, const uint8_t *gb
     }
 }
 
-__global__ void __launch_bounds__(kParseWG) k_dec_parse(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
-                                                    int32_t *status, uint32_t first, uint32_t count, BlkInfo *info,
-                                                    GroupRec *recs, uint32_t gmax, const uint32_t *order,
-                                                    uint32_t max_dsize) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG / 64) * kRingWave];
-    const uint32_t lane = threadIdx.x & 63;
-    uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWave;
-    const uint32_t lin = blockIdx.x * kParseWG + threadIdx.x;
-    const bool inrange = lin < count;
-    // block: the lin-th of the chunk's list (or of the call, in order); workspace slot: lin
-    const uint32_t i = inrange ? (order ? order[lin] : first + lin) : first;
-
-    int st = QLZX_OK;
-    uint32_t kind = kBlkSkip, csize = 0, dsize = 0, hdr = 0, len = 0;
-    const uint8_t *src = b.src + b.src_off[i];
-    if (inrange) {
-        len = b.src_len[i];
-        st = classify_block(src, len, dst_cap ? dst_cap[i] : 0xffffffffu, max_dsize, kind, csize, dsize, hdr);
-    }
-    const uintptr_t a = (uintptr_t)src;
-    const uint8_t *gbase = (const uint8_t *)(a & ~(uintptr_t)15);
-    const uint32_t shift = (uint32_t)(a & 15);
-    // bytes to stream: the compressed stream (stored blocks are copied by K2)
-    const uint32_t span = (st == QLZX_OK && kind == kBlkCompressed) ? csize : 0;
-    const uint32_t last16 = span ? (span + shift - 1) >> 4 : 0;
-    const uint32_t last_round = span ? (span + shift - 1) / kRoundBytes : 0;
-    bool stream = inrange && span > 0;
-    const bool parsing = stream && st == QLZX_OK && kind == kBlkCompressed;
-
-    // parse state
-    uint32_t ip = hdr, g = 0, k = 31, cw = 0, ra = 0, rb = 0, rec_ip = 0;
-#if !QLZX_K1_MLATE
-    uint32_t m = 0;
-#endif
-    GroupRec *myrec = recs + (size_t)(inrange ? lin : 0) * gmax;
-    bool done_parse = !parsing;
-
-    PROF_DECL
-    const uint8_t *dummy = (const uint8_t *)(((uintptr_t)b.src) & ~(uintptr_t)15);
-    ring_issue(ring, gbase, dummy, 0, last16, stream);
-    ring_issue(ring, gbase, dummy, 1, last16, stream && last_round >= 1);
-    ring_issue(ring, gbase, dummy, 2, last16, stream && last_round >= 2);
-    for (uint32_t r = 0;; r++) {
-        if (__ballot(stream && r <= last_round) == 0) break;
-        // rounds <= r landed once at most the newest two rounds' 8 DMAs are in flight
-        PROF_MARK(0);
-#if QLZX_K1_ROUND == 64
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-#elif QLZX_K1_ROUND == 32
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-#elif QLZX_K1_ROUND == 16
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-#else
-#error "QLZX_K1_ROUND: 16, 32 or 64"
-#endif
-        PROF_MARK(1);  // 1: waiting for the round's DMA
-        const bool act = stream && r <= last_round;
-        // parse while the bytes the next step reads have landed (stream pos < lim)
-        const uint32_t lim = (r + 1) * kRoundBytes - shift;
-        bool go = act && !done_parse;
-        while (__ballot(go)) {
-#ifdef QLZX_PROFILE
-            _pacc[5] += 1;
-            if (go) _pacc[6] += 1;
-#endif
-            // one step = a control word (k == 31), or a literal run (possibly empty)
-            // followed by the match that ends it.  Straight-line selects; only the
-            // record store branches.
-            const bool gb = k == 31;
-            const uint32_t kk = k & 31;
-            const uint32_t cwk = cw >> kk;
-            uint32_t run = __builtin_ctz(cwk | (1u << (31 - kk)));             // literals before the next match
-            run = gb ? 0u : (run < csize - ip ? run : csize - ip);
-            const uint32_t ipm = ip + run, km = kk + run;                       // the match after the run
-            const bool hasm = !gb & (km < 31) & (ipm < csize);
-            const bool end = ip + (gb ? 4u : 1u) > csize;                       // stream exhausted
-            const bool landed = ipm + (gb ? 4u : 1u) <= lim;                    // bytes this step reads
-            const bool mat = hasm & landed;
-            const bool stepping = go & !end & (gb ? landed : (run > 0) | mat);
-            const uint32_t w = ring_rd32(ring, ipm + shift, lane);  // cword, or the match token
-            const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
-            const uint32_t code = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);  // token bytes - 1
-            // a second match right after it when its first byte is already in w
-            const uint32_t ip2 = ipm + code + 1, k2 = km + 1;
-            const uint32_t w2 = w >> (8 * ((code + 1) & 3));
-#if QLZX_K1_NOMAT2
-            const bool mat2 = false;
-#else
-            const bool mat2 = mat & (code < 3) & (k2 < 31) & (((cw >> (k2 & 31)) & 1u) != 0) & (ip2 < csize) &
-                              (ip2 + 1 <= lim);
-#endif
-            const uint32_t ty2 = (w2 & 3u) + ((w2 & 127u) == 3u ? 1u : 0u);
-            const uint32_t code2 = __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4);
-            bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) |  // C1, group bound
-                                   (mat & (ipm + code + 1 > csize)) |        // C2
-                                   (mat2 & (ip2 + code2 + 1 > csize)));
-#if QLZX_K1_MLATE
-            // a group's match bits are its control word's (every item of a finished group is parsed)
-            if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, cw & 0x7fffffffu, ra, rb};
-#else
-            if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
-#endif
-            st = bad ? QLZX_E_CORRUPT : st;
-            const bool adv = stepping & !bad;
-            const bool ag = adv & gb;
-            const uint32_t bm = mat ? (1u << (km & 31)) : 0u;
-            const uint32_t bm2 = mat2 ? (1u << (k2 & 31)) : 0u;
-            rec_ip = ag ? ip : rec_ip;
-            cw = ag ? w : cw;
-            g += ag ? 1u : 0u;
-            ip += adv ? (gb ? 4u : run + (mat ? code + 1 : 0u) + (mat2 ? code2 + 1 : 0u)) : 0u;
-            k = adv ? (gb ? 0u : km + (mat ? 1u : 0u) + (mat2 ? 1u : 0u)) : k;
-#if !QLZX_K1_MLATE
-            m = adv ? (gb ? 0u : m | bm | bm2) : m;
-#endif
-            ra = adv ? (gb ? 0u : ra | ((code & 1u) ? bm : 0u) | ((code2 & 1u) ? bm2 : 0u)) : ra;
-            rb = adv ? (gb ? 0u : rb | ((code & 2u) ? bm : 0u) | ((code2 & 2u) ? bm2 : 0u)) : rb;
-            done_parse = done_parse | (go & (end | bad));
-            go = adv;
-        }
-        PROF_MARK(3);  // 3: parse
-        if (done_parse) stream = false;  // nothing left to read for this lane
-        // round r+3 reuses the slot of round r-1 (consumed: round r+1 reads only rounds r, r+1)
-        ring_issue(ring, gbase, dummy, r + 3, last16, stream && r + 3 <= last_round);
-    }
-    PROF_MARK(4);  // 4: DMA issue + loop overhead
-#if QLZX_K1_MLATE
-    if (parsing && st == QLZX_OK && g > 0)  // the last group: its first k items
-        myrec[g - 1] = GroupRec{rec_ip, cw & (k >= 31 ? 0x7fffffffu : ((1u << k) - 1u)), ra, rb};
-#else
-    if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, m, ra, rb};
-#endif
-    PROF_FLUSH(0);
-    vm_sync();
-    if (!inrange) return;
-    if (st == QLZX_OK && kind == kBlkCompressed && (!done_parse || g == 0)) st = QLZX_E_CORRUPT;
-    BlkInfo bi{0, 0, kind, dsize};
-    if (st != QLZX_OK) {
-        bi.kind = kBlkSkip;
-        status[i] = st;
-        if (dsize_out && st != kPending) dsize_out[i] = 0;
-    } else if (kind == kBlkCompressed) {
-        bi.ngroups = g;
-        bi.nitems = (g - 1) * 31 + (k > 31 ? 31 : k);
-    }
-    info[lin] = bi;
-}
-
-
-// --------------------------------------------- K2 helpers (qlzx_decode_bytes.hip) ----
+// ------------------------------------------------------------------- K2 helpers ----
 // Per-lane coordinates of item I = 64 bt + lane: group g = I / 31, index k = I % 31.
 // Advanced by one batch (64 = 2 * 31 + 2) without a division.
 struct ItemCursor {
@@ -408,35 +236,25 @@ __device__ __forceinline__ uint32_t ff1_or(uint64_t m, uint32_t dflt) {
     return m ? (uint32_t)__builtin_ctzll(m) : dflt;
 }
 
-}  // namespace qlzx
-#include "qlzx_decode_bytes.hip"
-namespace qlzx {
-
-#ifndef QLZX_K2B_WIN
-#define QLZX_K2B_WIN 4096
-#endif
-#ifndef QLZX_K2B_MR
-#define QLZX_K2B_MR 256
-#endif
-constexpr uint32_t kWinB = QLZX_K2B_WIN, kMarkRing = QLZX_K2B_MR;
+// Inclusive max over lanes 0..lane; DPP row shifts + row broadcasts.
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return v;
+}
+// Value of lane - 1 (0 in lane 0): DPP wave_shr:1.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
 
 }  // namespace qlzx
 #include "qlzx_decode_solo.hip"
 #include "qlzx_decode_small.hip"
 #include "qlzx_decode_v4.hip"
-#include "qlzx_decode_v5.hip"
-#ifndef QLZX_DEC_V5  // round-5 pair (k_dec_parse5 + k_dec_chunk5)
-#define QLZX_DEC_V5 0
-#endif
-#ifndef QLZX_DEC_V4
-#define QLZX_DEC_V4 1
-#endif
-#ifndef QLZX_K1_GLOBAL  // K1 reading the stream from global memory, no LDS ring (k_dec_parse_g)
-#define QLZX_K1_GLOBAL 0
-#endif
-#ifndef QLZX_K1_V3  // the round-3 K1 (a literal run and up to two matches per step) in front of the v4 K2
-#define QLZX_K1_V3 0
-#endif
 namespace qlzx {
 
 // Set by an atexit handler registered once the runtime is in use (after HIP registered its own
@@ -532,30 +350,18 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
         hipStream_t s1 = overlap ? side : s;
         if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
-        hipLaunchKernelGGL(QLZX_DEC_V5 ? k_dec_parse5 : QLZX_K1_GLOBAL ? k_dec_parse_g : ((QLZX_DEC_V4 && !QLZX_K1_V3) ? k_dec_parse4 : k_dec_parse),
+        hipLaunchKernelGGL(k_dec_parse4,
                            dim3((cnt + kParseWG - 1) / kParseWG),
                            dim3(kParseWG), 0, s1, b, dst_cap, dsize, status, first, cnt, info, recs, gmax, order,
                            max_dsize);
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
         // one kernel for every block size: the LDS window slides over longer blocks
-        if (QLZX_DEC_V5 && crc)
-            hipLaunchKernelGGL(k_dec_chunk5<true>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
-                               recs, gmax, (const uint32_t *)order, crc_state, crc_expect, crc_out);
-        else if (QLZX_DEC_V5)
-            hipLaunchKernelGGL(k_dec_chunk5<false>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
-                               recs, gmax, (const uint32_t *)order, nullptr, nullptr, nullptr);
-        else if (QLZX_DEC_V4 && crc)
+        if (crc)
             hipLaunchKernelGGL(k_dec_chunk4<true>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
                                recs, gmax, (const uint32_t *)order, crc_state, crc_expect, crc_out);
-        else if (QLZX_DEC_V4)
+        else
             hipLaunchKernelGGL(k_dec_chunk4<false>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
                                recs, gmax, (const uint32_t *)order, nullptr, nullptr, nullptr);
-        else if (crc)
-            hipLaunchKernelGGL((k_dec_bytes<kWinB, kMarkRing, true>), dim3(cnt), dim3(64), 0, s, b, dsize, status,
-                               first, cnt, info, recs, gmax, (const uint32_t *)order, crc_state, crc_expect, crc_out);
-        else
-            hipLaunchKernelGGL((k_dec_bytes<kWinB, kMarkRing, false>), dim3(cnt), dim3(64), 0, s, b, dsize, status,
-                               first, cnt, info, recs, gmax, (const uint32_t *)order, nullptr, nullptr, nullptr);
         if (overlap) (void)hipEventRecord(ev_k2[c & 1], s);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;

@@ -129,6 +129,7 @@ extern __device__ unsigned long long *g_prof;
         if (g_prof && (threadIdx.x & 63) == 0)                                      \
             for (int _j = 0; _j < 8; _j++) atomicAdd(&g_prof[(slot) * 8 + _j], _pacc[_j]); \
     } while (0)
+#define PROF_COUNT(i, v) (_pacc[i] += (v))
 #else
 #define PROF_DECL
 #define PROF_MARK(ph) \
@@ -137,6 +138,7 @@ extern __device__ unsigned long long *g_prof;
 #define PROF_FLUSH(slot) \
     do {                 \
     } while (0)
+#define PROF_COUNT(i, v) ((void)0)
 #endif
 
 // s_waitcnt on LDS only (no vmcnt), plus a compiler memory barrier.

@@ -65,16 +65,12 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t *lds, uint32_t a) {
 __device__ __forceinline__ uint32_t fetch24(const uint8_t *lds, uint32_t p) { return ld32u(lds, p) & 0xFFFFFFu; }
 __device__ __forceinline__ uint32_t hash12(uint32_t f) { return ((f >> 12) ^ f) & (QLZX_BUCKETS - 1); }
 
-#ifndef QLZX_ENC_PEERS_BITOP
-#define QLZX_ENC_PEERS_BITOP 1
-#endif
 // Lanes (within `act`) whose NB-bit key equals this lane's key.
 // Per key bit: an all-ones / zero lane mask from one sign-extending bit extract, the ballot of
 // it, and m &= ~(B ^ mask) on each 32-bit half (one three-input bit op each; the select form
 // `set ? B : ~B` compiled to nine VALU ops per bit).
 template <int NB>
 __device__ __forceinline__ uint64_t match_peers(uint32_t key, uint64_t act) {
-#if QLZX_ENC_PEERS_BITOP
     uint32_t lo = (uint32_t)act, hi = (uint32_t)(act >> 32);
 #pragma unroll
     for (int bi = 0; bi < NB; bi++) {
@@ -84,16 +80,6 @@ __device__ __forceinline__ uint64_t match_peers(uint32_t key, uint64_t act) {
         hi &= ~((uint32_t)(B >> 32) ^ sm);
     }
     return ((uint64_t)hi << 32) | lo;
-#else
-    uint64_t m = act;
-#pragma unroll
-    for (int bi = 0; bi < NB; bi++) {
-        const bool set = (key >> bi) & 1u;
-        const uint64_t B = __ballot(set);
-        m &= set ? B : ~B;
-    }
-    return m;
-#endif
 }
 
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t x, uint32_t d) {
@@ -180,58 +166,31 @@ constexpr uint32_t kEncGroups = 256;  // bucket groups (hash >> 4), 16 buckets e
 // 3/4 of the input + kPrefixMargin first.  On the c3 noisy blocks (40-45 % random bytes) 256 of
 // the 263 in 387 that end stored bail out at that first test, within 53 B of 3/4 of the input
 // (instrumented oracle), and D < 28 % flags them with 3 false positives.
-#ifndef QLZX_ENC_SPEC_COPY
-#define QLZX_ENC_SPEC_COPY 1
-#endif
-#ifndef QLZX_ENC_PREFIX
-#define QLZX_ENC_PREFIX 1
-#endif
-// Radix scatter: a lane's same-key peers from one 64-bit LDS OR per lane into a per-wave key slot
-// (read back, then cleared) instead of one ballot per key bit.
-#ifndef QLZX_ENC_LDS_PEERS
-#define QLZX_ENC_LDS_PEERS 0
-#endif
+constexpr bool kSpecCopy = true;
+constexpr bool kPrefixPass = true;
 // Best match in poorly compressible blocks (3-gram repeats, the stored proof's D, below
-// QLZX_ENC_COMPACT_PCT % of the positions; 0 = never): a wave whose lanes all have at most
+// kCompactPct % of the positions; 0 = never): a wave whose lanes all have at most
 // kMatchCompactMax candidates that can match (same 3 bytes, far enough back) visits only those,
 // in a per-lane bit loop, instead of all 16.
-#ifndef QLZX_ENC_COMPACT_PCT
-#define QLZX_ENC_COMPACT_PCT 60
-#endif
-#ifndef QLZX_ENC_MATCH_COMPACT
-#define QLZX_ENC_MATCH_COMPACT 10
-#endif
-constexpr uint32_t kMatchCompactMax = QLZX_ENC_MATCH_COMPACT;
+constexpr uint32_t kCompactPct = 60;
+constexpr uint32_t kMatchCompactN = 10;
+constexpr uint32_t kMatchCompactMax = kMatchCompactN;
 // Stored proof: 16-position steps per thread whose input loads are issued together.
-#ifndef QLZX_ENC_PROOF_STEPS
-#define QLZX_ENC_PROOF_STEPS 4
-#endif
+constexpr uint32_t kProofSteps = 4;
 // Bail-out after a parse: reuse the stored proof's speculative copy (only the edges written).
-#ifndef QLZX_ENC_BAIL_SPEC
-#define QLZX_ENC_BAIL_SPEC 1
-#endif
+constexpr bool kBailSpec = true;
 // Radix scatter: 64-element batches per iteration whose list loads are in flight together (the
 // second pass; the first reads no list).
-#ifndef QLZX_ENC_SCATTER_U
-#define QLZX_ENC_SCATTER_U 4
-#endif
+constexpr uint32_t kScatterU = 4;
 // Best match: sorted entries staged in LDS for this many consecutive 64-entry steps of a wave per
 // global-load wait (1 = one step per wait, the steps of a wave T entries apart).
-#ifndef QLZX_ENC_MATCH_STAGE
-#define QLZX_ENC_MATCH_STAGE 4
-#endif
+constexpr uint32_t kMatchStage = 4;
 // Bucket starts of the 64 KiB kernel in LDS (8 KiB) rather than in the workgroup's global slot.
-#ifndef QLZX_ENC_BST_LDS
-#define QLZX_ENC_BST_LDS 1
-#endif
-#ifndef QLZX_ENC_PREFIX_PCT
-#define QLZX_ENC_PREFIX_PCT 28
-#endif
-#ifndef QLZX_ENC_PREFIX_MARGIN
-#define QLZX_ENC_PREFIX_MARGIN 1024
-#endif
-constexpr uint32_t kPrefixMinLen = QLZX_ENC_PREFIX ? 16384 : 0xFFFFFFFFu, kPrefixRepeatPct = QLZX_ENC_PREFIX_PCT,
-                   kPrefixMargin = QLZX_ENC_PREFIX_MARGIN;
+constexpr bool kBstLds = true;
+constexpr uint32_t kPrefixPct = 28;
+constexpr uint32_t kPrefixMarginB = 1024;
+constexpr uint32_t kPrefixMinLen = kPrefixPass ? 16384 : 0xFFFFFFFFu, kPrefixRepeatPct = kPrefixPct,
+                   kPrefixMargin = kPrefixMarginB;
 constexpr uint32_t kParseRounds = 4;  // segment-walker rounds before the serial item walk
 
 // One pass of a stable LSD radix partition of the searched positions by
@@ -254,11 +213,10 @@ __device__ __forceinline__ uint32_t cslot(uint32_t L) {
 }
 constexpr uint32_t cslots(uint32_t nkeys, uint32_t W) { return nkeys * (W + 1); }
 
-//   pe        (LP) per-wave 256-slot u64 LDS array, all zero on entry and on exit
-template <uint32_t W, uint32_t NB_LOG2, bool LP, typename OUT>
+template <uint32_t W, uint32_t NB_LOG2, typename OUT>
 __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t *in, OUT *out, uint32_t shift,
                                  uint32_t *cnt, uint64_t *wsum, unsigned long long *sub, uint32_t *hist,
-                                 uint32_t *next_cnt, bool counted, unsigned long long *pe) {
+                                 uint32_t *next_cnt, bool counted) {
 #ifdef QLZX_PROFILE
 #define SUB_MARK(k)                                                         \
     do {                                                                    \
@@ -279,7 +237,7 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
     const uint32_t per = (P + 64 * W - 1) / (64 * W) * 64;
     const uint32_t r0 = min(P, wave * per), r1 = min(P, r0 + per);
     const uint32_t per_magic = 0xFFFFFFFFu / per + 1u;  // umulhi(x, per_magic) = x / per for x < 2^16
-    constexpr uint32_t U = sizeof(OUT) == 4 ? QLZX_ENC_SCATTER_U : 4;  // 64-element batches per iteration
+    constexpr uint32_t U = sizeof(OUT) == 4 ? kScatterU : 4;  // 64-element batches per iteration
     SUB_MARK(0);
     if (!counted) {
         for (uint32_t k = tid; k < cslots(NB, W); k += T) cnt[k] = 0;
@@ -339,28 +297,14 @@ __device__ void stable_partition(const uint8_t *s_in, uint32_t P, const uint16_t
         const uint32_t f = fetch24(s_in, p);
         const uint32_t h = hash12(f);
         const uint32_t key = valid ? (h >> shift) & (NB - 1) : 0u;
-        uint64_t peers;
-        if constexpr (LP) {
-            // in-order LDS per wave: every lane's OR lands before any lane's read, every read
-            // before any lane's clear
-            unsigned long long *ps = pe + wave * 256 + key;
-            if (valid) __hip_atomic_fetch_or(ps, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            peers = valid ? *(volatile unsigned long long *)ps : 0ull;
-            if (valid) *(volatile unsigned long long *)ps = 0ull;
-        } else {
-            peers = match_peers<NB_LOG2>(key, __ballot(valid));
-        }
+        const uint64_t peers = match_peers<NB_LOG2>(key, __ballot(valid));
         const uint32_t intra = __popcll(peers & ltm);
         uint32_t cur = 0;
         if (valid) cur = cnt[cslot<W>(key * W + wave)];
         // every lane's read is issued before the leader's write (in-order LDS per wave)
         if (valid && intra == 0) cnt[cslot<W>(key * W + wave)] = cur + (uint32_t)__popcll(peers);
         if (valid) {
-#ifdef QLZX_EXP_SCATTER_LINEAR  // timing experiment only (wrong output): stores in input order
-            out[sizeof(OUT) == 4 ? j : cur + intra] = (OUT)(sizeof(OUT) == 2 ? p : p | ((f >> 12) << 16));
-#else
             out[cur + intra] = (OUT)(sizeof(OUT) == 2 ? p : p | ((f >> 12) << 16));
-#endif
             if (next_cnt) atomicAdd(&next_cnt[cslot<W>((h >> 4) * W + __umulhi(cur + intra, per_magic))], 1u);
         }
       }
@@ -382,14 +326,10 @@ __device__ void bucket_sort(const uint8_t *s_in, uint32_t P, uint16_t *tmp, uint
     const uint32_t tid = tid_here();
     uint32_t *cntB = s_cnt, *cntA = s_cnt + cslots(kEncGroups, W);
     // LDS peer slots after the histogram, where the workgroup's LDS has room for them
-    constexpr bool LP = QLZX_ENC_LDS_PEERS && L8_BYTES >= QLZX_BUCKETS * 2 + W * 256 * 8;
-    unsigned long long *pe = (unsigned long long *)(s_hist + QLZX_BUCKETS / 2);
-    if constexpr (LP)
-        for (uint32_t k = tid; k < W * 256; k += T) pe[k] = 0ull;
     for (uint32_t k = tid; k < QLZX_BUCKETS / 2; k += T) s_hist[k] = 0;
     for (uint32_t k = tid; k < cslots(kEncGroups, W); k += T) cntB[k] = 0;
     // (pass A zeroes its own counters and syncs before counting)
-    stable_partition<W, 4, LP>(s_in, P, nullptr, tmp, 0, cntA, wsum, subA, s_hist, cntB, false, pe);
+    stable_partition<W, 4>(s_in, P, nullptr, tmp, 0, cntA, wsum, subA, s_hist, cntB, false);
     // bucket starts: exclusive scan of the u16-pair histogram, bucket order = sorted order
     {
         constexpr uint32_t PT = QLZX_BUCKETS / 2 / T > 0 ? QLZX_BUCKETS / 2 / T : 1;  // words per thread
@@ -414,7 +354,7 @@ __device__ void bucket_sort(const uint8_t *s_in, uint32_t P, uint16_t *tmp, uint
 #ifdef QLZX_PROFILE
     if (subB) subB[7] = __builtin_amdgcn_s_memtime();
 #endif
-    stable_partition<W, 8, LP>(s_in, P, tmp, gl, 4, cntB, wsum, subB, nullptr, nullptr, true, pe);
+    stable_partition<W, 8>(s_in, P, tmp, gl, 4, cntB, wsum, subB, nullptr, nullptr, true);
 }
 
 template <uint32_t CAP>
@@ -455,7 +395,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
     __shared__ __attribute__((aligned(16))) uint32_t s_scr[C::SCR];
     __shared__ uint64_t s_wsum[W];
     __shared__ uint32_t s_misc[24];  // [0] next group, [1] proof count, [4..] CRC stripes
-    constexpr bool BL = QLZX_ENC_BST_LDS && CAP == 65536;  // (the smaller kernels' occupancy is LDS-bound)
+    constexpr bool BL = kBstLds && CAP == 65536;  // (the smaller kernels' occupancy is LDS-bound)
     __shared__ uint16_t s_bst[BL ? QLZX_BUCKETS : 1];
     uint8_t *const s_in = s_u, *const s_l8 = s_u + C::IN_B;
 
@@ -503,15 +443,15 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             for (uint32_t k = tid * 4; k < BMW; k += T * 4) *(uint4 *)(bm + k) = make_uint4(z0, z0, z0, z0);
             __syncthreads();
             const uint32_t ny = n - 2;  // positions holding a whole 3-gram
-            auto load20 = [&](uint32_t y0, uint32_t w[6]) {  // w[5] only with QLZX_ENC_SPEC_COPY
+            auto load20 = [&](uint32_t y0, uint32_t w[6]) {  // w[5] only with kSpecCopy
                 if (y0 + 24 <= n) {
                     const uint4 v = *(const uint4 *)(src + y0);
                     w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
                     w[4] = *(const uint32_t *)(src + y0 + 16);
-                    if (QLZX_ENC_SPEC_COPY) w[5] = *(const uint32_t *)(src + y0 + 20);
+                    if (kSpecCopy) w[5] = *(const uint32_t *)(src + y0 + 20);
                 } else {
 #pragma unroll
-                    for (int j = 0; j < (QLZX_ENC_SPEC_COPY ? 6 : 5); j++) {
+                    for (int j = 0; j < (kSpecCopy ? 6 : 5); j++) {
                         uint32_t x = 0;
                         for (int k = 0; k < 4; k++) {
                             const uint32_t o = y0 + 4 * j + k;
@@ -547,7 +487,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             // value (header + input: chunk o holds input bytes o - 9 ..) go out now, each from the
             // window of the step 16 bytes before it.  A block that is not stored overwrites them
             // (its output is shorter; dst capacity is >= n + 400).
-            spec = QLZX_ENC_SPEC_COPY && hdr == 9 && (((uintptr_t)dst) & 15u) == 0;
+            spec = kSpecCopy && hdr == 9 && (((uintptr_t)dst) & 15u) == 0;
             const uint32_t sa1 = (n + hdr) & ~15u;
             auto spec16 = [&](uint32_t y0, const uint32_t w[6]) {
                 if (spec && y0 + 32 <= sa1)
@@ -555,9 +495,9 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                         __builtin_amdgcn_alignbyte(w[2], w[1], 3), __builtin_amdgcn_alignbyte(w[3], w[2], 3),
                         __builtin_amdgcn_alignbyte(w[4], w[3], 3), __builtin_amdgcn_alignbyte(w[5], w[4], 3));
             };
-            // QLZX_ENC_PROOF_STEPS 16-position steps per iteration (4: a whole block of any class
+            // kProofSteps 16-position steps per iteration (4: a whole block of any class
             // in one iteration), every load in flight before any step is hashed
-            constexpr uint32_t PS = QLZX_ENC_PROOF_STEPS;
+            constexpr uint32_t PS = kProofSteps;
             for (uint32_t y0 = tid * 16; y0 < ny; y0 += PS * T * 16) {
                 uint32_t w[PS][6];
 #pragma unroll
@@ -587,7 +527,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
             // poorly compressible but not provably stored (the c3 noisy blocks): likely to bail out
             // at the first control word past 3/4 of the input, so try the prefix alone first
             prefix = !stored && n >= kPrefixMinLen && 100ull * (ny - s_misc[1]) < (uint64_t)kPrefixRepeatPct * ny;
-            cmode = !stored && 100ull * (ny - s_misc[1]) < (uint64_t)QLZX_ENC_COMPACT_PCT * ny;
+            cmode = !stored && 100ull * (ny - s_misc[1]) < (uint64_t)kCompactPct * ny;
             if (stored) {  // quicklz.c:722-727 from the global copy of the input
                 QLZX_TID_REFRESH();
                 if ((((uintptr_t)dst) & 15u) == 0) {
@@ -672,9 +612,9 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 // memory once per wave-iteration into an 80-word LDS stage (s_scr is free between
                 // the sort and the parse) and the 16 candidate reads per position are LDS reads
                 // of consecutive words, not 16 global loads.
-                // With QLZX_ENC_MATCH_STAGE = S > 1 a wave takes S consecutive steps (64 S entries)
+                // With kMatchStage = S > 1 a wave takes S consecutive steps (64 S entries)
                 // at a time: their S + 1 list loads are issued together and waited for once.
-                constexpr uint32_t S = QLZX_ENC_MATCH_STAGE, SW = 64 * S + 16;
+                constexpr uint32_t S = kMatchStage, SW = 64 * S + 16;
                 static_assert(C::SCR >= SW * W, "candidate stage");
                 uint32_t *const stg0 = s_scr + wave * SW;
                 auto best_matches = [&](auto compact) {
@@ -958,7 +898,7 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     const uint32_t tot = n + hdr, a0 = (hdr + 15u) & ~15u, a1 = tot & ~15u;
                     // a bail-out emits nothing before this point, so after a speculative copy
                     // only the edges are missing
-                    for (uint32_t o = a0 + tid * 16; o < (spec && QLZX_ENC_BAIL_SPEC ? a0 : a1); o += T * 16) {
+                    for (uint32_t o = a0 + tid * 16; o < (spec && kBailSpec ? a0 : a1); o += T * 16) {
                         const uint32_t q = o - hdr;
                         *(uint4 *)(dst + o) = make_uint4(ld32u(s_in, q), ld32u(s_in, q + 4), ld32u(s_in, q + 8),
                                                          ld32u(s_in, q + 12));

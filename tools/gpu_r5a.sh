@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/${OUT:-r05a}; mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+QLZX_LIB=$PWD/${TEST_LIB:-gobeansdb_amd/libqlzx.so} timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
     tests/test_gpu_codec.py tests/test_gpu_sample_parity.py ${EXTRA_TESTS} 2>&1 | tail -30 | tee $O/tests.txt
 [ ${PIPESTATUS[0]} -ne 0 ] && exit 1
 : > $O/ab.txt

@@ -1,7 +1,7 @@
 """HBM traffic per block of the decode kernels from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
 
 usage: python tools/traffic.py gpurun_out/TAG NBLOCKS OUT.json [KERNEL_SUBSTRINGS]
-KERNEL_SUBSTRINGS: comma-separated kernel-name filters (default "k_dec_parse,k_dec_bytes";
+KERNEL_SUBSTRINGS: comma-separated kernel-name filters (default "k_dec_parse,k_dec_chunk";
 "k_encode_wg" for the c3 encoder).
 FETCH_SIZE/WRITE_SIZE are KiB per dispatch.  Per MI355X_MICROARCH.md (HBM section)
 FETCH_SIZE counts half the bytes of 16-B-per-lane streaming reads on gfx950, so it
@@ -15,7 +15,7 @@ import sys
 from collections import defaultdict
 
 root, nblocks, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
-pats = sys.argv[4].split(",") if len(sys.argv) > 4 else ["k_dec_parse", "k_dec_bytes"]
+pats = sys.argv[4].split(",") if len(sys.argv) > 4 else ["k_dec_parse", "k_dec_chunk"]
 per = defaultdict(lambda: defaultdict(float))  # (kernel, dispatch) -> counter -> value
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     with open(f) as fh:
