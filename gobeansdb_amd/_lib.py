@@ -115,6 +115,8 @@ def lib() -> ctypes.CDLL:
     L.qlzx_last_error.restype = ctypes.c_char_p
     L.qlzx_info.argtypes = [ctypes.c_char_p, sz]
     L.qlzx_info.restype = ctypes.c_int
+    L.qlzx_service_test_fault.argtypes = [ctypes.c_int]
+    L.qlzx_service_test_fault.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -824,6 +824,14 @@ extern "C" {
 
 int qlzx_last_status(void) { return t_last_status; }
 
+int qlzx_service_test_fault(int mode) {
+    if (mode != 1 && mode != 2) return fail(QLZX_R_BAD_ARG, "qlzx_service_test_fault: mode is 1 or 2");
+    Service *S = service();
+    if (!S) return QLZX_R_NO_DEVICE;
+    S->fault.store(mode, std::memory_order_release);
+    return QLZX_R_OK;
+}
+
 size_t qlz_compress(const void *source, char *destination, size_t size, char *scratch_compress) {
     (void)scratch_compress;
     if (size == 0 || size > 0xffffffffull - 400) return 0;  // quicklz.c:705-706

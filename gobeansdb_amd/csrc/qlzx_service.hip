@@ -11,7 +11,10 @@
 //   * each kernel stages its request in (host slot -> HBM), runs the op, stages the result out
 //     (HBM -> host slot) and, after a system-scope release, stores the request's sequence number
 //     into its host-visible completion word.  The caller spins on that word (no stream
-//     synchronisation, no event), copies its result out and frees the slot.
+//     synchronisation), copies its result out and frees the slot;
+//   * every batch also records an event after its kernels; a spinning caller polls it now and then
+//     (hipEventQuery), so a batch that ends without publishing, or a stream in error, fails its
+//     requests with QLZX_R_HIP instead of leaving the callers spinning.
 // Launches rotate over kSvcStreams streams, so a batch launched while an earlier one still runs
 // does not queue behind it.  Values above kSvcMaxLen (and the Go-compat encoder modes) take the
 // general per-call path in qlzx_api.hip.
@@ -145,6 +148,11 @@ __global__ void __launch_bounds__(256) k_svc_enc_out(SvcBatch B, uint8_t *h_aren
     svc_publish(done, r, n, st, 0);
 }
 
+// test hook (qlzx_service_test_fault): a batch that runs but never publishes its completions
+__global__ void k_svc_nop(uint32_t *sink) {
+    if (sink && threadIdx.x == 0) *sink = 0;
+}
+
 }  // namespace qlzx
 
 namespace {
@@ -180,11 +188,19 @@ struct Service {
     std::atomic<uint32_t> inflight{0};     // launched, completion not yet seen by the caller
     std::atomic<int64_t> oldest_ns{0};     // when the oldest pending request was queued
     uint32_t next_stream = 0;
+    // Batch events: a batch holds one from launch until every caller in it (and the leader) has
+    // let go.  Each held event maps to a held slot, so kSvcSlots of them never run out for long.
+    hipEvent_t ev[kSvcSlots] = {};
+    std::atomic<int32_t> ev_refs[kSvcSlots] = {};
+    std::atomic<uint64_t> ev_free{~0ull};
+    std::atomic<uint64_t> slot_ev[kSvcSlots] = {};  // seq << 32 | (event index + 1), set after the record
+    std::atomic<int> fault{0};                      // test hook, consumed by the next launch
 
     int init(int device) {
         dev = device;
         HIP_OK(hipSetDevice(device));
         for (auto &s : st) HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        for (auto &e : ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIP_OK(hipHostMalloc((void **)&h_arena, kSvcSlots * qlzx::kSvcHostSlot + kSvcSlots * sizeof(qlzx::SvcDone),
                              hipHostMallocCoherent | hipHostMallocMapped));
         h_done = (qlzx::SvcDone *)(h_arena + kSvcSlots * qlzx::kSvcHostSlot);
@@ -194,6 +210,31 @@ struct Service {
         for (auto &w : d_enc_ws) HIP_OK(hipMalloc((void **)&w, enc_ws_bytes));
         ok = true;
         return 0;
+    }
+    // undo a partial init (service() keeps the failure, it never retries)
+    void release() {
+        for (auto &w : d_enc_ws)
+            if (w) (void)hipFree(w), w = nullptr;
+        if (d_arena) (void)hipFree(d_arena), d_arena = nullptr;
+        if (h_arena) (void)hipHostFree(h_arena), h_arena = nullptr;
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e), e = nullptr;
+        for (auto &s : st)
+            if (s) (void)hipStreamDestroy(s), s = nullptr;
+    }
+
+    uint32_t take_ev() {
+        for (uint32_t spins = 0;; spins++) {
+            uint64_t m = ev_free.load(std::memory_order_relaxed);
+            while (m) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                if (ev_free.compare_exchange_weak(m, m & ~(1ull << b), std::memory_order_acquire)) return b;
+            }
+            if (spins > 64) std::this_thread::yield(); else _mm_pause();
+        }
+    }
+    void drop_ev(uint32_t e) {
+        if (ev_refs[e].fetch_sub(1, std::memory_order_acq_rel) == 1) ev_free.fetch_or(1ull << e, std::memory_order_release);
     }
 
     uint32_t take_slot() {
@@ -212,6 +253,8 @@ struct Service {
 
     // Launch everything queued (the caller is the leader).  Returns a qlzx_return code.
     int launch(std::vector<SvcPending> &batch) {
+        const int inj = fault.exchange(0, std::memory_order_acq_rel);
+        if (inj == 2) return fail(QLZX_R_HIP, "service launch (injected failure)");
         qlzx::SvcBatch B[qlzx::kSvcOps];
         for (auto &b : B) b.n = 0;
         for (const auto &p : batch) B[p.op].r[B[p.op].n++] = p.r;
@@ -222,6 +265,10 @@ struct Service {
             const uint32_t k = next_stream++ % kSvcStreams;
             s = st[k];
             ws = d_enc_ws[k];
+        }
+        if (inj == 1) {  // the batch runs, publishes nothing and completes its event
+            hipLaunchKernelGGL(qlzx::k_svc_nop, dim3(1), dim3(64), 0, s, (uint32_t *)nullptr);
+            for (auto &b : B) b.n = 0;
         }
         if (B[qlzx::kSvcDecode].n)
             hipLaunchKernelGGL(qlzx::k_svc_decode, dim3(B[qlzx::kSvcDecode].n), dim3(qlzx::kSoloWG), 0, s,
@@ -240,13 +287,47 @@ struct Service {
             hipLaunchKernelGGL(qlzx::k_svc_enc_out, dim3(n), dim3(256), 0, s, B[qlzx::kSvcCompress], h_arena,
                                (const uint8_t *)d_arena, (const qlzx::SvcEncDesc *)desc, h_done);
         }
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return fail(QLZX_R_HIP, "service launch", e);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(s);  // whatever did launch is done before its slots are failed
+            return fail(QLZX_R_HIP, "service launch", e);
+        }
+        // the batch event: one reference per request plus the leader's until the slots know it
+        const uint32_t k = take_ev();
+        ev_refs[k].store((int32_t)batch.size() + 1, std::memory_order_relaxed);
+        e = hipEventRecord(ev[k], s);
+        if (e != hipSuccess) {
+            ev_refs[k].store(1, std::memory_order_relaxed);
+            drop_ev(k);
+            (void)hipStreamSynchronize(s);
+            return fail(QLZX_R_HIP, "service event record", e);
+        }
+        for (const auto &p : batch) slot_ev[p.r.slot].store(tag(p.r.seq, k), std::memory_order_release);
+        drop_ev(k);
         return QLZX_R_OK;
+    }
+    static constexpr uint32_t kNoEv = 0xffffffffu;  // slot_ev for a batch that failed to launch
+    static uint64_t tag(uint32_t seq, uint32_t k) { return (uint64_t)seq << 32 | (k == kNoEv ? kNoEv : k + 1); }
+
+    // A caller's check on its own batch (every ~1K spins): 0 while it may still complete, else a
+    // qlzx_return code.  `held` is the batch event this caller references (-1 until it is known).
+    int check(uint32_t slot, uint32_t seq, volatile qlzx::SvcDone *d, int32_t *held) {
+        if (*held < 0) {
+            const uint64_t v = slot_ev[slot].load(std::memory_order_acquire);
+            if ((uint32_t)(v >> 32) != seq || (uint32_t)v == 0 || (uint32_t)v == kNoEv) return 0;  // not yet
+            *held = (int32_t)(uint32_t)v - 1;
+        }
+        const hipError_t q = hipEventQuery(ev[*held]);
+        if (q == hipErrorNotReady) return 0;
+        if (q != hipSuccess) return fail(QLZX_R_HIP, "service batch", q);
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (d->seq == seq) return 0;  // published after all; the loop sees it
+        return fail(QLZX_R_HIP, "service batch ended without completing the request");
     }
 
     // Queue one request and wait for it.  On a launch failure every request of that batch is
-    // completed with status -1 (the callers then report QLZX_R_HIP).
+    // completed with status -1 (the callers then report QLZX_R_HIP); a batch that ends without
+    // publishing, or whose stream reports an error, fails the same way through its event.
     int run(uint32_t op, qlzx::SvcReq r) {
         r.seq = ++seq[r.slot];  // the slot is this thread's until give_slot
         volatile qlzx::SvcDone *d = h_done + r.slot;
@@ -257,7 +338,9 @@ struct Service {
             npending.fetch_add(1, std::memory_order_release);
         }
         int rc = QLZX_R_OK;
+        int32_t held = -1;  // this request's batch event, once launched
         for (uint32_t spins = 0; d->seq != r.seq; spins++) {
+            if ((spins & 1023) == 1023 && (rc = check(r.slot, r.seq, d, &held)) != QLZX_R_OK) break;
             const uint32_t np = npending.load(std::memory_order_acquire);
             if (!leading.load(std::memory_order_acquire) && np &&
                 (inflight.load(std::memory_order_acquire) == 0 || np >= qlzx::kSvcBatchTarget ||
@@ -280,6 +363,7 @@ struct Service {
                             volatile qlzx::SvcDone *x = h_done + p.r.slot;
                             x->status = -1;
                             x->seq = p.r.seq;
+                            slot_ev[p.r.slot].store(tag(p.r.seq, kNoEv), std::memory_order_release);
                         }
                         rc = lr;
                     }
@@ -289,15 +373,29 @@ struct Service {
             }
             if (spins > 20000) std::this_thread::yield(); else _mm_pause();
         }
+        // The leader always tags the request's slot after the launch (event or kNoEv); wait for
+        // that, so the slot is not handed on while the leader may still write to it.  (A request
+        // can be published before its leader gets there.)
+        if (held < 0)
+            for (uint32_t w = 0;; w++) {
+                const uint64_t v = slot_ev[r.slot].load(std::memory_order_acquire);
+                if ((uint32_t)(v >> 32) == r.seq && (uint32_t)v) {
+                    if ((uint32_t)v != kNoEv) held = (int32_t)(uint32_t)v - 1;
+                    break;
+                }
+                if (w > 64) std::this_thread::yield(); else _mm_pause();
+            }
+        if (held >= 0) drop_ev((uint32_t)held);
         std::atomic_thread_fence(std::memory_order_acquire);
         inflight.fetch_sub(1, std::memory_order_acq_rel);
-        if (d->status == -1 && rc == QLZX_R_OK) rc = fail(QLZX_R_HIP, "service launch failed (another caller's batch)");
+        if (rc == QLZX_R_OK && d->status == -1) rc = fail(QLZX_R_HIP, "service launch failed (another caller's batch)");
         return rc;
     }
 };
 
 Service *service() {
     static Service *svc[qlzx::kMaxDevices] = {};
+    static std::string init_err[qlzx::kMaxDevices];  // sticky: a failed init is not retried
     static std::mutex init_mu;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= (int)qlzx::kMaxDevices) {
@@ -312,8 +410,18 @@ Service *service() {
             fail(QLZX_R_NO_DEVICE, "no HIP device");
             return nullptr;
         }
+        if (!init_err[dev].empty()) {
+            fail(QLZX_R_NO_DEVICE, init_err[dev].c_str());
+            return nullptr;
+        }
         auto *s = new Service();
-        if (s->init(dev) != 0) return nullptr;  // leaked on purpose: a half-made service is never reused
+        if (s->init(dev) != 0) {
+            init_err[dev] = "service init failed earlier: " + t_last_error;
+            s->release();
+            delete s;
+            fail(QLZX_R_NO_DEVICE, init_err[dev].c_str());
+            return nullptr;
+        }
         __atomic_store_n(&svc[dev], s, __ATOMIC_RELEASE);
     }
     return svc[dev];

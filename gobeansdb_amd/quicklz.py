@@ -136,9 +136,16 @@ def Decompress(source) -> bytes:
     L = _lib.lib()
     if level == 3 and (s[0] & 1):
         # qlz_decompress reads SizeCompressed(s) bytes (quicklz.c:777-836 trusts the header);
-        # Go indexes source[] and panics once it runs past len(source) (quicklz.go:291-431)
+        # Go never reads that field: it decodes any stream whose tokens fit in len(source) and
+        # panics on the first index past it (quicklz.go:291-431).  A header csize above len(s)
+        # is therefore rewritten to len(s): the decoder is then bounded exactly where Go is.
         if len(s) < SizeCompressed(s):
-            raise QuicklzError(f"truncated quicklz stream: {len(s)} bytes < header csize {SizeCompressed(s)}")
+            b = bytearray(s)
+            if s[0] & 2:
+                b[1:5] = len(s).to_bytes(4, "little")
+            else:
+                b[1] = len(s)
+            s = bytes(b)
         size = L.qlz_decompress(s, dst, None)
         bad = size != n or L.qlzx_last_status() != _lib.OK
     else:

@@ -32,14 +32,27 @@ class ReplayResult:
     flag: torch.Tensor         # int32 [n] flag after Payload.Decompress
     value_len: torch.Tensor    # int32 [n] value length after decompress
     vhash: torch.Tensor        # int32 [n] Getvhash of the value (uint16)
-    values: batch.BlockBatch   # decompressed values (compressed records) / raw bodies (others)
+    # The FLAG_COMPRESS records only, in record order: their decoder outputs in one packed buffer
+    # (lengths = the QuickLZ header dsize, meaningless for a record whose decode failed).  Read a
+    # record's value through in_out / val_off (or value(j)), not by position in here.
+    values: batch.BlockBatch
     end_error: bool            # the reader stopped on an unexpected EOF after these records
     n_candidates: int
     n_valid: int
+    in_out: torch.Tensor       # uint8 [n]: 1 = value in values.data at val_off, 0 = in the chunk at val_off
+    val_off: torch.Tensor      # int64 [n] value offset (decoded buffer or chunk, per in_out)
+    data: torch.Tensor         # the chunk replayed (val_off's base where in_out is 0)
 
     @property
     def n(self) -> int:
         return int(self.offset.numel())
+
+    def value(self, j: int) -> bytes:
+        """Record j's value after Payload.Decompress (store/item.go:163-176): the decoded bytes, or
+        the raw body where the record is not compressed or its decode failed."""
+        o, n = int(self.val_off[j]), int(self.value_len[j])
+        src = self.values.data if int(self.in_out[j]) else self.data
+        return src[o:o + n].cpu().numpy().tobytes()
 
 
 def index(data: torch.Tensor, start: int = 0, max_key: int = MAX_KEY_LEN, body_max: int = BODY_MAX,
@@ -120,10 +133,8 @@ def replay(data: torch.Tensor, start: int = 0, max_key: int = MAX_KEY_LEN, body_
                                     in_out.data_ptr(), val_off.data_ptr(), vh16.data_ptr(), st_),
                "qlzx_replay_finish")
     vh = vh16[:n].to(torch.int32) & 0xFFFF
-    res = ReplayResult(rec_off[:n], rec_broken[:n], hdr[: 6 * n].view(n, 6), flag[:n], value_len[:n], vh, values,
-                       bool(r[1]), int(r[2]), int(r[3]))
-    res.in_out, res.val_off = in_out[:n], val_off[:n]
-    return res
+    return ReplayResult(rec_off[:n], rec_broken[:n], hdr[: 6 * n].view(n, 6), flag[:n], value_len[:n], vh, values,
+                        bool(r[1]), int(r[2]), int(r[3]), in_out[:n], val_off[:n], data)
 
 
 class _nullctx:

@@ -104,7 +104,15 @@ typedef struct qlzx_blocks {
  *                above the fast-path limit take the general kernel).  A block whose
  *                header dsize exceeds it is not decoded: status QLZX_E_MAX_DSIZE.
  * The record CRC is computed over the compressed bytes in the same pass that
- * decodes them (fused). */
+ * decodes them (fused).
+ * Values over 64 KiB (max_dsize > 65536): the batch decoder decodes every block up to 64 KiB
+ * asynchronously, then each larger block in its own whole-GPU pass, one block at a time; that
+ * phase reads counts back and synchronises `stream` several times per large block, so the call
+ * returns only after it (blocks up to 64 KiB never do).  The workspace then also holds the
+ * whole-GPU decoder's scratch: about 31.7 x max_dsize bytes (8 u16 jump levels over 1.5 x
+ * max_dsize plus a u32 source index per output byte), e.g. 1.66 GB at the 50 MiB body limit.
+ * qlzx_decompress_workspace_size includes it; size max_dsize from the largest header dsize
+ * actually pending (as replay does), not from a configured bound. */
 size_t qlzx_decompress_workspace_size(uint32_t n, uint32_t max_dsize);
 int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_t *dsize,
                           int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
@@ -120,7 +128,11 @@ int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_
  *   status[i]    out: enum qlzx_status                           (nullable)
  *   crc_state / crc_out: as above, over the *compressed* output (the value
  *   bytes of the record written by store/datafile.go:307-330).  Fused.
- *   max_len      upper bound on src_len over the batch */
+ *   max_len      upper bound on src_len over the batch
+ * Values over 64 KiB (max_len > 65536) are encoded by a whole-GPU pass each, one at a time,
+ * after the batch's smaller blocks; like the decoder, that phase synchronises `stream` several
+ * times per large block, and the workspace grows by about 76 x max_len bytes (jump levels, sort
+ * keys and scans; 3.99 GB at 50 MiB), included in qlzx_compress_workspace_size. */
 #define QLZX_F_GO_COMPAT 1u /* Go quicklz.Compress(src, 3) output (quicklz.go:80-289): always a
                               9-byte header, bail-out counts the header, no 9-byte core minimum */
 size_t qlzx_compress_workspace_size(uint32_t n, uint32_t max_len);
@@ -235,8 +247,15 @@ int qlzx_last_status(void);
 /* Last error message of the calling thread (empty if none). */
 const char *qlzx_last_error(void);
 
-/* Library/version info: fills `buf` with a short description (arch, kernels). */
+/* Library/version info: fills `buf` with a short description (arch, kernels, source hash). */
 int qlzx_info(char *buf, size_t len);
+
+/* Test hook for the request path behind the drop-ins (values <= 64 KiB): the next batch the
+ * current device's service launches fails -- mode 1: its kernel runs but publishes no
+ * completion (caught through the batch event), mode 2: the launch itself fails.  Every request
+ * of that batch then fails with QLZX_R_HIP (qlzx_compress1 returns 0, the quicklz.h drop-ins
+ * stop the process).  Returns a qlzx_return code. */
+int qlzx_service_test_fault(int mode);
 
 #ifdef __cplusplus
 }

@@ -355,3 +355,26 @@ def test_go_decompress1_error_channel(cuda):
             assert r == _lib.GO_ERROR and L.qlzx_last_status() == want
             with pytest.raises(QuicklzError):
                 Decompress(s)
+
+
+def test_decompress_inflated_header_csize_decodes_like_go(cuda):
+    """Go's Decompress never reads SizeCompressed (quicklz.go:291-431): a valid stream whose header
+    csize is larger than the buffer decodes, and one whose tokens run past the buffer panics.
+    The mirror bounds the decoder by len(s) (the header is rewritten), pinned by the oracle on
+    the same rewritten stream."""
+    import struct
+    from gobeansdb_amd.quicklz import Decompress, QuicklzError
+    for n in (100, 5000, 70000):
+        v = O.gen_text(31, n, n)
+        c = O.compress(v)
+        assert c[0] & 1
+        hdr = 9 if c[0] & 2 else 3
+        if hdr == 9:
+            inflated = c[:1] + struct.pack("<I", len(c) + 1000) + c[5:]
+        else:
+            inflated = c[:1] + bytes([min(255, len(c) + 50)]) + c[2:]
+        assert O.decompress(c)[1] == v  # the oracle on the stream bounded by its length
+        assert Decompress(inflated) == v
+        cut = inflated[:len(c) - 7]  # tokens run past the buffer: Go panics
+        with pytest.raises(QuicklzError):
+            Decompress(cut)

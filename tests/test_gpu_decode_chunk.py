@@ -1,10 +1,10 @@
-"""GPU parity for the byte-parallel K2 (k_dec_bytes, qlzx_decode_bytes.hip) on inputs built
-to stress its three mechanisms, against the oracle-compressed stream of the same input:
+"""GPU parity for the byte-parallel K2 (k_dec_chunk4, qlzx_decode_v4.hip) on inputs built to
+stress its three mechanisms, against the oracle-compressed stream of the same input:
 
 * in-chunk sources resolved by pointer jumping: periodic data (short periods give chains of
   dozens of bytes inside one 256-B chunk; 255/256/257 straddle the chunk size);
-* the LDS window boundary: periods and back-references just below / at / above the window
-  size minus the marker ring (near vs far source);
+* the 4 KiB LDS window boundary: periods and back-references just below / at / above the
+  window size and the window minus a chunk (near vs far source);
 * far sources read back from HBM, ragged block ends (dsize not a multiple of 4 or 256) and
   tiny blocks.
 """

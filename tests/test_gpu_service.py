@@ -70,3 +70,30 @@ def test_service_concurrent_callers(cuda):
         t.join(timeout=240)
     assert not any(t.is_alive() for t in threads), "a caller did not return"
     assert errors == [], errors[:5]
+
+
+@pytest.mark.parametrize("mode,msg", [(1, "ended without completing"), (2, "injected failure")])
+def test_service_batch_failure_is_reported(cuda, mode, msg):
+    """A batch whose kernel runs but publishes nothing (mode 1, caught through the batch event)
+    or whose launch fails (mode 2) fails its request with QLZX_R_HIP instead of leaving the
+    caller spinning; the next request is served normally (no slot or event left behind)."""
+    from gobeansdb_amd import _lib
+    L = _lib.lib()
+    v = O.gen_text(7, 0, 3000)
+    dst = ctypes.create_string_buffer(len(v) + 400)
+    assert L.qlzx_compress1(v, dst, len(v), 0) == len(O.compress(v))  # the service is up
+    assert L.qlzx_service_test_fault(mode) == 0
+    result = []
+    t = threading.Thread(target=lambda: result.append(L.qlzx_compress1(v, dst, len(v), 0)))
+    t.start()
+    t.join(timeout=60)
+    assert not t.is_alive(), "the failed request did not return"
+    assert result == [0]
+    # qlzx_last_error is per thread: repeat on this thread for the message
+    assert L.qlzx_service_test_fault(mode) == 0
+    assert L.qlzx_compress1(v, dst, len(v), 0) == 0
+    assert msg in L.qlzx_last_error().decode()
+    for _ in range(3 * 64):  # more than the slot and event pools: nothing leaked
+        n = L.qlzx_compress1(v, dst, len(v), 0)
+        assert dst.raw[:n] == O.compress(v)
+    assert L.qlzx_service_test_fault(3) != 0
