@@ -14,10 +14,11 @@ Prints one JSON line (rank 0).  See DESIGN.md §3 for the roofline accounting.  
 run (1 M x 16 KiB) also measures BASELINE config c3 -- compress + fused CRC32 of 1 M x 64 KiB
 image-like values, the "(+compress)" of the metric -- after releasing the c2 buffers, and reports
 it under "compress" in the same line (--no-c3 skips it; --config c3 runs it alone); then config c4
--- .data replay of two distinct chunk files, device-resident and pipelined end to end -- under
-"replay" (--no-c4 skips it); then config c5
--- 400 GiB of mixed 4-64 KiB values split over the ranks, strong scaling -- under "mixed"
-(--no-c5 skips it; --config c5 runs it alone).
+-- .data replay of one ~50 GiB corpus of chunk files split over the ranks on record boundaries,
+device-resident and pipelined end to end -- under "replay" (--no-c4 skips it); then config c5
+-- one 400 GiB corpus of distinct mixed 4-64 KiB values split over the ranks and streamed through
+HBM in rounds, strong scaling -- under "mixed" (--no-c5 skips it; --config c5 runs it alone).
+c4 and c5 carry a parity digest (XOR of output CRC32s, all-gathered) that is the same at every N.
 """
 from __future__ import annotations
 
@@ -76,7 +77,7 @@ def parse():
     p.add_argument("--no-c4", action="store_true",
                    help="c2 run: skip the c4 .data replay leg reported under \"replay\" in the same line")
     p.add_argument("--c4-chunk-mib", type=int, default=4000, help="c4 leg: MiB per chunk file (two distinct)")
-    p.add_argument("--c4-files", type=int, default=13, help="c4 leg: files replayed end to end (~50 GiB)")
+    p.add_argument("--c4-files", type=int, default=13, help="c4 leg: files in the corpus (~50 GiB)")
     p.add_argument("--crc", action="store_true", help="fused record CRC verify in the timed pass")
     p.add_argument("--no-crc-leg", action="store_true",
                    help="skip the \"crc\" leg (the c2 shard again with the fused CRC verify)")
@@ -318,14 +319,14 @@ def main():
         comp = bench_compress(a3, rank, world, dev, "image", emit=False)
     replay_rec = None
     if not args.no_c4 and legs:
-        # BASELINE config c4: .data replay (scan + CRC + decompress + vhash), device-resident and
-        # end to end from pinned host memory, two distinct chunk files per rank
+        # BASELINE config c4: .data replay (scan + CRC + decompress + vhash) of one corpus split over
+        # the ranks on record boundaries, device-resident and end to end from pinned host memory
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import bench_replay as c4mod
         a4 = argparse.Namespace(chunk_mib=256 if args.legs_small else args.c4_chunk_mib,
-                                files=4 if args.legs_small else args.c4_files, steps=4, seed=2026,
+                                files=4 if args.legs_small else args.c4_files, steps=2, seed=2026,
                                 cpu_seconds=max(2.0, args.cpu_seconds / 2), no_cpu=args.no_cpu,
                                 pin_records=64 if args.legs_small else 1024)
         replay_rec = c4mod.run(a4, rank, world, dev)
@@ -333,8 +334,8 @@ def main():
         torch.cuda.empty_cache()
     mixed = None
     if not args.no_c5 and legs:
-        # BASELINE config c5 in the same run: 400 GiB of mixed 4-64 KiB values split over the
-        # ranks (strong scaling), so the driver's 1/2/4/8-GPU runs also measure it
+        # BASELINE config c5 in the same run: one 400 GiB corpus of distinct mixed 4-64 KiB values
+        # split over the ranks (strong scaling), so the driver's 1/2/4/8-GPU runs also measure it
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -350,7 +351,7 @@ def main():
             rec["replay"] = replay_rec
         if mixed is not None:
             rec["mixed"] = {k: mixed[k] for k in ("metric", "value", "unit", "scaling", "rounds_per_gpu", "wall_s",
-                                                  "config", "roofline")}
+                                                  "incl_h2d", "digest", "config", "roofline")}
             if world == 1 and not args.no_cpu:  # CPU leg at N = 1 only, like the other legs
                 rec["mixed"]["cpu_baseline"] = cpu_baseline_mixed(max(2.0, args.cpu_seconds / 2))
         print(json.dumps(rec), flush=True)

@@ -198,8 +198,10 @@ def crc32(src: BlockBatch, init: torch.Tensor | None = None, final_xor: int = 0x
 _TABLES_DEV = {}
 
 
-def synth(kind: str, seed: int, lengths, first_id: int = 0, device="cuda", stream=None) -> BlockBatch:
-    """Deterministic synthetic blocks generated on the GPU."""
+def synth(kind: str, seed: int, lengths, first_id: int = 0, device="cuda", stream=None,
+          out: BlockBatch | None = None) -> BlockBatch:
+    """Deterministic synthetic blocks generated on the GPU: block i is
+    gen(seed, first_id + i), written into `out` (its offsets and lengths) when given."""
     from . import synth as S
     L = _lib.lib()
     key = str(device)
@@ -208,7 +210,8 @@ def synth(kind: str, seed: int, lengths, first_id: int = 0, device="cuda", strea
         _TABLES_DEV[key] = (torch.from_numpy(v).to(device), torch.from_numpy(o.view(np.int32)).to(device),
                             torch.from_numpy(c.view(np.int32)).to(device))
     v, o, c = _TABLES_DEV[key]
-    out = BlockBatch.empty_for(lengths, device=device)
+    if out is None:
+        out = BlockBatch.empty_for(lengths, device=device)
     rc = L.qlzx_synth_batch(0 if kind == "text" else 1, seed, first_id, out.data.data_ptr(), out.off.data_ptr(),
                             out.length.data_ptr(), out.n, v.data_ptr(), o.data_ptr(), c.data_ptr(), c.numel(),
                             _stream(stream))

@@ -54,6 +54,16 @@ class ReplayResult:
         src = self.values.data if int(self.in_out[j]) else self.data
         return src[o:o + n].cpu().numpy().tobytes()
 
+    def value_crcs(self, stream=None) -> torch.Tensor:
+        """crc32 (store/crc32.go get) of every record's value after Payload.Decompress, on the
+        device (int32 [n]); an XOR of them is the parity digest of a replay."""
+        out = torch.zeros(self.n, dtype=torch.int32, device=self.offset.device)
+        for where, src in ((1, self.values.data), (0, self.data)):
+            m = torch.nonzero(self.in_out == where).flatten()
+            if m.numel():
+                out[m] = batch.crc32(batch.BlockBatch(src, self.val_off[m], self.value_len[m]), stream=stream)
+        return out
+
 
 def index(data: torch.Tensor, start: int = 0, max_key: int = MAX_KEY_LEN, body_max: int = BODY_MAX,
           workspace: batch.Workspace | None = None, stream=None):

@@ -52,12 +52,26 @@ def test_main_does_not_shadow_module_functions():
     assert not (local & top), f"main() shadows module functions: {sorted(local & top)}"
 
 
-def test_c5_rounds_total_400_gib_at_every_n():
-    """bench's c5 leg (tools/bench_c5.py) is strong scaling: the job is 400 GiB at N = 1..8."""
+def test_c5_one_corpus_split_into_distinct_rounds_at_every_n():
+    """bench's c5 leg (tools/bench_c5.py) is strong scaling over ONE corpus: 400 GiB of blocks
+    drawn from one seed, split over the ranks by bytes, each share cut into rounds of at most
+    16 GiB; at every N the rounds of all ranks tile the corpus once (no block decoded twice)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import numpy as np
     import bench_c5
+    from gobeansdb_amd import shard
+    sizes, is_text = bench_c5.corpus(400.0)
+    assert sizes.sum() >= 400 * 2**30 and sizes[:-1].sum() < 400 * 2**30
+    assert sizes.min() >= 4096 and sizes.max() <= 65536
+    assert abs(is_text.mean() - 0.7) < 0.01
+    s2, t2 = bench_c5.corpus(400.0)
+    assert np.array_equal(sizes, s2) and np.array_equal(is_text, t2)   # the same on every rank
     for world in (1, 2, 4, 8):
-        rounds, target = bench_c5.plan_rounds(400.0, 16.0, world)
-        assert target <= 16 * 2**30
-        assert abs(rounds * target * world - 400 * 2**30) <= world * rounds
-    assert bench_c5.plan_rounds(400.0, 16.0, 1) == (25, 16 * 2**30)
+        covered = []
+        for lo, hi in shard.partition_by_bytes(sizes, world):
+            rounds = bench_c5.plan_rounds(sizes, lo, hi, 16.0)
+            assert all(int(sizes[a:b].sum()) <= 16 * 2**30 + 65536 for a, b in rounds)
+            covered += rounds
+        assert covered[0][0] == 0 and covered[-1][1] == len(sizes)
+        assert all(x[1] == y[0] for x, y in zip(covered, covered[1:]))
+        assert len(covered) <= 25 + world

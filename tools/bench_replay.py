@@ -2,17 +2,18 @@
 """Config c4: replay a synthetic .data corpus on one GPU, device-only and end-to-end.
 
 A chunk file (store/datafile.go layout: 24-B header, key, value, 256-B padding)
-of --chunk-mib MiB is built once from synthetic values (log-uniform 4-64 KiB,
+of --chunk-mib MiB is built from synthetic values (log-uniform 4-64 KiB,
 70 % text / 30 % image-like).  Values pass the TryCompress policy of store/item.go:120-161:
 the MIME sniff of the first 512 B (gobeansdb_amd.record.need_compress), a trial compress
 of the first 10 KiB kept when float32(clen)/float32(tlen) <= 0.7, then the whole body.
 Keys are "key_%016x".
-Two such chunks are built from distinct seeds; --files files alternating them (13 x 4000 MiB
-~ 50 GiB by default) are replayed:
+Two such chunks are built from distinct seeds; the corpus is --files files alternating them
+(13 x 4000 MiB ~ 50 GiB by default), split over the ranks on record boundaries:
 
-  device-only   the chunk is resident in HBM; one step = qlzx_replay_index +
-                decompress of FLAG_COMPRESS values + Getvhash (gobeansdb_amd.replay)
-  end-to-end    pipelined per file: pinned H2D of the chunk, the same replay, D2H of
+  device-only   the chunks are resident in HBM; one step = every rank replays its share
+                (qlzx_replay_index + decompress of FLAG_COMPRESS values + Getvhash,
+                gobeansdb_amd.replay) once
+  end-to-end    pipelined per piece: pinned H2D of the piece, the same replay, D2H of
                 the decompressed values into pinned host memory, three streams
 
 The CPU leg runs the reference record loop (crc32_write + qlz_decompress + Getvhash from
@@ -181,16 +182,23 @@ def committed_traffic(step_chunk_bytes: float, path: str = C4_TRAFFIC) -> dict:
 
 
 def run(a, rank: int, world: int, dev):
-    """c4 on this rank: two distinct chunk files (seeds a.seed + 2 rank and + 1), each built,
-    replayed once against its expected record set, then timed device-only (steps alternate the
-    two resident chunks) and end to end from pinned host memory (a.files files alternating the
-    two chunks, so consecutive files are different bytes).  Returns the rank's record (rank 0:
-    max-over-ranks times and summed bytes; the CPU leg at N = 1 only)."""
+    """c4 on this rank.  The job is ONE corpus: a.files .data files alternating two distinct
+    chunk files (seeds a.seed and a.seed + 1, the same on every rank), ~50 GiB at the defaults.
+    It is split over the ranks on record boundaries by bytes (shard.partition_data_files, SURVEY
+    §8(e)); a rank replays only its byte ranges, each a .data stream of its own.
+    * gate (untimed): both chunks replayed whole against their expected record sets and
+      `pin_records` sampled records against the oracle; then every piece of this rank replayed
+      once: its record count, no resync, and the XOR of its value CRCs (all-gathered into the
+      corpus digest, the same at every N);
+    * device-only: the rank's pieces from the resident chunks, a.steps passes;
+    * end to end: the same pieces pipelined from pinned host memory (H2D of piece i+1, replay of
+      piece i, D2H of piece i-1's decompressed values on three streams).
+    Returns the record on rank 0 (max-over-ranks times, summed bytes; CPU leg at N = 1 only)."""
     from gobeansdb_amd import replay, batch, shard
     t0 = time.time()
     chunks = []
     for j in range(2):
-        host, nrec, stored_bytes, raw_bytes, rec_off = build_chunk(a.chunk_mib, a.seed + 2 * rank + j, dev)
+        host, nrec, stored_bytes, raw_bytes, rec_off = build_chunk(a.chunk_mib, a.seed + j, dev)
         chunks.append(dict(host=host, nrec=nrec, raw=raw_bytes, rec_off=rec_off,
                            pinned=torch.from_numpy(host).pin_memory()))
     log(f"rank {rank}: two chunks built in {time.time() - t0:.1f}s: "
@@ -206,10 +214,33 @@ def run(a, rank: int, world: int, dev):
         assert int(res.value_len.to(torch.int64).sum()) == c["raw"], "decompressed sizes"
         assert int(((res.flag & 0x10000) != 0).sum()) == 0, "a compressed value failed to decode"
         c["compressed"] = int(((res.header[:, 2] & 0x10000) != 0).sum())
-        c["out_cap"] = res.values.data.numel()
         c["pinned_sample"] = pin_sample(c, res, getattr(a, "pin_records", 1024))
         del res
     log("replay verified: all records, all values decoded, both chunks")
+
+    # ---- the corpus and this rank's share (the generated files have no gaps: every record
+    # start is a cut point) ----
+    corpus = [f & 1 for f in range(a.files)]
+    plan = shard.partition_data_files([(chunks[k]["rec_off"], len(chunks[k]["host"])) for k in corpus], world)
+    pieces = [(corpus[f], lo, hi) for f, lo, hi in plan[rank]]
+    digest, nrec_mine, out_mine, out_cap = 0, 0, 0, 0
+    for f, lo, hi in plan[rank]:
+        c = chunks[corpus[f]]
+        ro = c["rec_off"].astype(np.int64)
+        want = int(np.searchsorted(ro, hi) - np.searchsorted(ro, lo))
+        res = replay.replay(c["dev"][lo:hi], workspace=ws)
+        torch.cuda.synchronize()
+        assert res.n == want and not res.end_error and int(res.size_broken.abs().sum()) == 0, (res.n, want)
+        # the corpus repeats its two chunk files, so each record's CRC is keyed by its place
+        # (file, offset) before the XOR: a repeated record does not cancel itself out
+        pos = res.offset.to(torch.int64) + lo
+        key = (pos * 0x85EBCA77 + (f + 1) * 0x9E3779B1) & 0xFFFFFFFF
+        digest ^= shard.xor_of((res.value_crcs().to(torch.int64) & 0xFFFFFFFF) ^ key)
+        nrec_mine += res.n
+        out_mine += int(res.value_len.to(torch.int64).sum())
+        out_cap = max(out_cap, res.values.data.numel())
+        del res
+    digest = shard.xor_digest_over_ranks(digest, device=dev)
     stream = torch.cuda.current_stream(dev)
 
     def sync_all():
@@ -218,91 +249,107 @@ def run(a, rank: int, world: int, dev):
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
-    # ---- device-only: the chunk resident in HBM ----
-    replay.replay(chunks[0]["dev"], workspace=ws)
+    # ---- device-only: the rank's pieces from the resident chunks ----
+    if pieces:
+        k, lo, hi = pieces[0]
+        replay.replay(chunks[k]["dev"][lo:hi], workspace=ws)
     sync_all()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t = time.perf_counter()
     e0.record(stream)
-    for k in range(a.steps):
-        replay.replay(chunks[k & 1]["dev"], workspace=ws, stream=stream)
+    for _ in range(a.steps):
+        for k, lo, hi in pieces:
+            replay.replay(chunks[k]["dev"][lo:hi], workspace=ws, stream=stream)
     e1.record(stream)
     sync_all()
     dev_wall = time.perf_counter() - t
     dev_ev = e0.elapsed_time(e1) * 1e-3
-    chunk_b = [len(c["host"]) for c in chunks]
-    steps_chunk = sum(chunk_b[k & 1] for k in range(a.steps))
-    steps_out = sum(chunks[k & 1]["raw"] for k in range(a.steps))
+    share = sum(hi - lo for _, lo, hi in pieces)
 
-    # ---- end to end, pipelined: H2D of file i+1 || replay of file i || D2H of file i-1 ----
-    # three streams, two device chunk slots and two pinned output slots (PCIe is full duplex);
-    # only decompressed values travel back (raw values are bytes the host already holds)
-    cap = max(c["out_cap"] for c in chunks)
+    # ---- end to end, pipelined: H2D of piece i+1 || replay of piece i || D2H of piece i-1 ----
+    # three streams, two device slots and two pinned output slots (PCIe is full duplex); only
+    # decompressed values travel back (raw values are bytes the host already holds)
+    slot_b = max([hi - lo for _, lo, hi in pieces], default=1)
     s_h2d, s_cmp, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    dslot = [chunks[0]["dev"], chunks[1]["dev"]]
-    hslot = [torch.empty(cap, dtype=torch.uint8).pin_memory() for _ in range(2)]
-    ev_in = [torch.cuda.Event(), torch.cuda.Event()]      # chunk landed in slot
+    dslot = [torch.empty(slot_b, dtype=torch.uint8, device=dev) for _ in range(2)]
+    hslot = [torch.empty(max(out_cap, 1), dtype=torch.uint8).pin_memory() for _ in range(2)]
+    ev_in = [torch.cuda.Event(), torch.cuda.Event()]      # piece landed in slot
     ev_used = [torch.cuda.Event(), torch.cuda.Event()]    # replay done with slot
     ev_out = [torch.cuda.Event(), torch.cuda.Event()]     # D2H done with host slot
+
+    def h2d(i):
+        k, lo, hi = pieces[i]
+        dslot[i & 1][: hi - lo].copy_(chunks[k]["pinned"][lo:hi], non_blocking=True)
+        ev_in[i & 1].record(s_h2d)
+
     sync_all()
     t = time.perf_counter()
-    with torch.cuda.stream(s_h2d):
-        dslot[0][: chunk_b[0]].copy_(chunks[0]["pinned"], non_blocking=True)
-        ev_in[0].record(s_h2d)
-    e2e_bytes = 0
-    for i in range(a.files):
-        k = i & 1
-        n_i = chunk_b[k]
-        e2e_bytes += n_i
-        if i + 1 < a.files:   # prefetch the next file (the other chunk) while this one replays
+    if pieces:
+        with torch.cuda.stream(s_h2d):
+            h2d(0)
+    for i, (k, lo, hi) in enumerate(pieces):
+        j = i & 1
+        if i + 1 < len(pieces):   # prefetch the next piece while this one replays
             with torch.cuda.stream(s_h2d):
                 if i >= 1:
-                    s_h2d.wait_event(ev_used[k ^ 1])
-                dslot[k ^ 1].copy_(chunks[k ^ 1]["pinned"], non_blocking=True)
-                ev_in[k ^ 1].record(s_h2d)
+                    s_h2d.wait_event(ev_used[j ^ 1])
+                h2d(i + 1)
         with torch.cuda.stream(s_cmp):
-            s_cmp.wait_event(ev_in[k])
-            r = replay.replay(dslot[k], workspace=ws, stream=s_cmp)
-            ev_used[k].record(s_cmp)
+            s_cmp.wait_event(ev_in[j])
+            r = replay.replay(dslot[j][: hi - lo], workspace=ws, stream=s_cmp)
+            ev_used[j].record(s_cmp)
         with torch.cuda.stream(s_d2h):
-            s_d2h.wait_event(ev_used[k])
+            s_d2h.wait_event(ev_used[j])
             if i >= 2:
-                s_d2h.wait_event(ev_out[k])
+                s_d2h.wait_event(ev_out[j])
             nb = r.values.data.numel()
-            hslot[k][:nb].copy_(r.values.data, non_blocking=True)
+            hslot[j][:nb].copy_(r.values.data, non_blocking=True)
             r.values.data.record_stream(s_d2h)
-            ev_out[k].record(s_d2h)
+            ev_out[j].record(s_d2h)
     sync_all()
     pipe_s = time.perf_counter() - t
     dev_wall, dev_ev, pipe_s = shard.max_over_ranks([dev_wall, dev_ev, pipe_s], device=dev)
-    tot = shard.sum_over_ranks({"chunk": steps_chunk, "out": steps_out, "e2e": e2e_bytes}, device=dev)
+    tot = shard.sum_over_ranks({"chunk": share, "out": out_mine, "records": nrec_mine, "pieces": len(pieces)},
+                               device=dev)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(chunks[0]["host"], chunks[0]["rec_off"], a.cpu_seconds)
     if rank != 0:
         return None
-    achieved = (tot["chunk"] + tot["out"]) / world / a.steps / (dev_ev / a.steps) / 1e9
+    achieved = (tot["chunk"] + tot["out"]) / world / (dev_ev / a.steps) / 1e9
+    corpus_b = sum(len(chunks[k]["host"]) for k in corpus)
     return {
         "metric": "GiB/s .data replay (record scan + CRC + decompress + vhash), c4",
-        "value": round(tot["chunk"] / dev_wall / 2**30, 2), "unit": "GiB/s of chunk, device-resident",
+        "value": round(tot["chunk"] * a.steps / dev_wall / 2**30, 2), "unit": "GiB/s of chunk, device-resident",
         "ms_per_step": round(dev_wall * 1e3 / a.steps, 3), "steps": a.steps,
-        "config": {"workload": f"c4: two distinct {a.chunk_mib} MiB .data chunk files per GPU "
-                               "(store/datafile.go layout, log-uniform 4-64 KiB values, 70 % text, TryCompress "
-                               "policy), replayed as buildHintFromData reads them (store/bucket.go:89-117)",
+        "scaling": "strong",
+        "config": {"workload": f"c4: one corpus of {a.files} .data files ({corpus_b / 2**30:.1f} GiB: two distinct "
+                               f"{a.chunk_mib} MiB chunk files alternating; store/datafile.go layout, log-uniform "
+                               "4-64 KiB values, 70 % text, TryCompress policy) split over the ranks on record "
+                               "boundaries (shard.partition_data_files), replayed as buildHintFromData reads them "
+                               "(store/bucket.go:89-117); a step = every rank replays its share once",
                    "records_per_chunk": [c["nrec"] for c in chunks],
                    "oracle_pinned_records": [c["pinned_sample"] for c in chunks],
                    "compressed_values": [c["compressed"] for c in chunks],
-                   "chunk_bytes": chunk_b, "parallelism": f"shard{world}"},
-        "values_out_gib_per_s": round(tot["out"] / dev_wall / 2**30, 2),
+                   "chunk_bytes": [len(c["host"]) for c in chunks], "corpus_bytes": corpus_b,
+                   "pieces": tot["pieces"], "parallelism": f"shard{world}"},
+        "digest": {"records": tot["records"], "value_bytes": tot["out"],
+                   "xor_value_crc32": f"{digest:08x}",
+                   "what": "XOR over every record of the corpus of crc32 (store/crc32.go) of its value after "
+                           "Payload.Decompress, keyed by the record's place ((offset * 0x85EBCA77 + (file + 1) * "
+                           "0x9E3779B1) mod 2^32, XORed in) since the corpus repeats its two chunk files; per-rank "
+                           "XORs all-gathered: equal at every N"},
+        "values_out_gib_per_s": round(tot["out"] * a.steps / dev_wall / 2**30, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), **committed_traffic(steps_chunk / a.steps),
-                     "what": "per step: every chunk byte read once (scan + CRC) + every value byte written",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), **committed_traffic(tot["chunk"] / world),
+                     "what": "per rank and step: every chunk byte of its share read once (scan + CRC) + every "
+                             "value byte written",
                      "kernel_ms": round(dev_ev * 1e3 / a.steps, 3)},
-        "end_to_end_pipelined": {"files": a.files, "total_gib": round(tot["e2e"] / 2**30, 2),
-                                 "gib_per_s_chunk": round(tot["e2e"] / pipe_s / 2**30, 2),
+        "end_to_end_pipelined": {"total_gib": round(tot["chunk"] / 2**30, 2),
+                                 "gib_per_s_chunk": round(tot["chunk"] / pipe_s / 2**30, 2),
                                  "seconds": round(pipe_s, 2),
-                                 "note": "files alternate the two chunks; pinned H2D of file i+1, replay of file i "
-                                         "and pinned D2H of file i-1's decompressed values on three streams"},
+                                 "note": "each rank's pieces: pinned H2D of piece i+1, replay of piece i and pinned "
+                                         "D2H of piece i-1's decompressed values on three streams"},
         "data": "synthetic",
         "cpu_baseline": cpu,
     }
