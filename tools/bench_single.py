@@ -6,8 +6,12 @@ These are the calls store/ makes per value: CCompress once or twice per set
 CDecompressSafe per get (store/item.go:167).  Every call goes through ctypes on both sides,
 so the Python call overhead (~1 us) is in both columns.  The reference column "cgo" also
 allocates a 528,400-B scratch and the output buffer per call, as cquicklz.go:24-34 does.
+Each size has --values DISTINCT text values (1024 by default) and consecutive calls take the
+next one, on both sides: no call repeats the previous call's value, so neither side gets a
+warmed branch predictor or cache from decoding one value in a loop.
 
-usage: python tools/bench_single.py [--calls 300] [--out profiles/r02_single_call.json]
+usage: python tools/bench_single.py [--calls 1000] [--values 1024] [--out FILE] [--dump DIR]
+  --dump DIR writes DIR/values_<n>.bin for tools/mt_single.c
 """
 from __future__ import annotations
 
@@ -63,8 +67,10 @@ def aggregate(fn_for_thread, threads, seconds):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--calls", type=int, default=300)
+    ap.add_argument("--calls", type=int, default=1000)
+    ap.add_argument("--values", type=int, default=1024, help="distinct values per size")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--dump", default=None, help="write values_<n>.bin (tools/mt_single.c input) here")
     ap.add_argument("--threads", type=int, default=16, help="aggregate-throughput callers (0: skip)")
     ap.add_argument("--seconds", type=float, default=3.0)
     a = ap.parse_args()
@@ -74,50 +80,75 @@ def main():
     ref = O.ref()
     rows = []
     for n in (4096, 16384, 65536):
-        plain = O.gen_text(0x5EED2026, n, n)
-        comp = O.compress(plain)
-        src = np.frombuffer(plain, np.uint8).copy()
-        csrc = np.frombuffer(comp, np.uint8).copy()
+        plains = [O.gen_text(0x5EED2026 + n, i, n) for i in range(a.values)]
+        comps = [O.compress(p) for p in plains]
+        if a.dump:
+            import struct
+            with open(os.path.join(a.dump, f"values_{n}.bin"), "wb") as f:
+                for c, p in zip(comps, plains):
+                    f.write(struct.pack("<II", len(c), len(p)) + c + p)
+        src = [np.frombuffer(p, np.uint8).copy() for p in plains]
+        csrc = [np.frombuffer(c, np.uint8).copy() for c in comps]
         dst = np.zeros(n + 400, np.uint8)
         scratch = np.zeros(528400, np.uint8)
-        # correctness of both sides before timing
-        assert L.qlz_compress(src.ctypes.data, dst.ctypes.data, n, scratch.ctypes.data) == len(comp)
-        assert dst[:len(comp)].tobytes() == comp
-        assert L.qlz_decompress(csrc.ctypes.data, dst.ctypes.data, scratch.ctypes.data) == n
-        assert dst[:n].tobytes() == plain
-        assert L.crc32_write(0xFFFFFFFF, src.ctypes.data, n) == O.crc32_write(0xFFFFFFFF, plain)
-        row = {"bytes": n, "ratio": round(len(comp) / n, 3)}
-        row["gpu_compress_us"] = med_us(lambda: L.qlz_compress(src.ctypes.data, dst.ctypes.data, n, 0), a.calls)
+        # correctness of the GPU side on every value before timing
+        for k in range(a.values):
+            assert L.qlz_compress(src[k].ctypes.data, dst.ctypes.data, n, scratch.ctypes.data) == len(comps[k])
+            assert dst[:len(comps[k])].tobytes() == comps[k]
+            assert L.qlz_decompress(csrc[k].ctypes.data, dst.ctypes.data, scratch.ctypes.data) == n
+            assert dst[:n].tobytes() == plains[k]
+            assert L.crc32_write(0xFFFFFFFF, src[k].ctypes.data, n) == O.crc32_write(0xFFFFFFFF, plains[k])
+        row = {"bytes": n, "values": a.values, "ratio": round(sum(map(len, comps)) / (n * a.values), 3)}
+        nv = a.values
+
+        def cyc(f):
+            """f(k) over the values in turn"""
+            state = [0]
+
+            def g():
+                k = state[0]
+                state[0] = k + 1 if k + 1 < nv else 0
+                f(k)
+            return g
+
+        row["gpu_compress_us"] = med_us(cyc(lambda k: L.qlz_compress(src[k].ctypes.data, dst.ctypes.data, n, 0)),
+                                        a.calls)
         pct = {}
-        row["gpu_decompress_us"] = med_us(lambda: L.qlz_decompress(csrc.ctypes.data, dst.ctypes.data, 0), a.calls,
-                                          pct)
+        row["gpu_decompress_us"] = med_us(cyc(lambda k: L.qlz_decompress(csrc[k].ctypes.data, dst.ctypes.data, 0)),
+                                          a.calls, pct)
         row["gpu_decompress_p99_us"] = pct["p99"]
-        row["gpu_crc32_us"] = med_us(lambda: L.crc32_write(0xFFFFFFFF, src.ctypes.data, n), a.calls)
+        row["gpu_crc32_us"] = med_us(cyc(lambda k: L.crc32_write(0xFFFFFFFF, src[k].ctypes.data, n)), a.calls)
         if ref is not None:
             Q, C = ref
 
-            def cgo_compress():
+            def cgo_compress(k):
                 sc = np.empty(528400, np.uint8)
                 out = np.empty(n + 400, np.uint8)
-                Q.qlz_compress(src.ctypes.data, out.ctypes.data, n, sc.ctypes.data)
+                Q.qlz_compress(src[k].ctypes.data, out.ctypes.data, n, sc.ctypes.data)
 
-            def cgo_decompress():
+            def cgo_decompress(k):
                 out = np.empty(n, np.uint8)
-                Q.qlz_decompress(csrc.ctypes.data, out.ctypes.data, scratch.ctypes.data)
+                Q.qlz_decompress(csrc[k].ctypes.data, out.ctypes.data, scratch.ctypes.data)
 
-            row["ref_compress_us"] = med_us(lambda: Q.qlz_compress(src.ctypes.data, dst.ctypes.data, n,
-                                                                   scratch.ctypes.data), a.calls)
-            row["ref_compress_cgo_us"] = med_us(cgo_compress, a.calls)
-            row["ref_decompress_us"] = med_us(lambda: Q.qlz_decompress(csrc.ctypes.data, dst.ctypes.data,
-                                                                       scratch.ctypes.data), a.calls)
-            row["ref_decompress_cgo_us"] = med_us(cgo_decompress, a.calls)
-            row["ref_crc32_us"] = med_us(lambda: C.crc32_write(0xFFFFFFFF, src.ctypes.data, n), a.calls)
+            row["ref_compress_us"] = med_us(cyc(lambda k: Q.qlz_compress(src[k].ctypes.data, dst.ctypes.data, n,
+                                                                         scratch.ctypes.data)), a.calls)
+            row["ref_compress_cgo_us"] = med_us(cyc(cgo_compress), a.calls)
+            row["ref_decompress_us"] = med_us(cyc(lambda k: Q.qlz_decompress(csrc[k].ctypes.data, dst.ctypes.data,
+                                                                             scratch.ctypes.data)), a.calls)
+            row["ref_decompress_cgo_us"] = med_us(cyc(cgo_decompress), a.calls)
+            row["ref_crc32_us"] = med_us(cyc(lambda k: C.crc32_write(0xFFFFFFFF, src[k].ctypes.data, n)), a.calls)
         if a.threads:
             def mk(lib):
                 def for_thread(t):
                     out = np.zeros(n + 64, np.uint8)
                     sc = np.zeros(528400, np.uint8)
-                    return lambda: lib.qlz_decompress(csrc.ctypes.data, out.ctypes.data, sc.ctypes.data)
+                    state = [t * nv // a.threads]
+
+                    def call():
+                        k = state[0]
+                        state[0] = k + 1 if k + 1 < nv else 0
+                        lib.qlz_decompress(csrc[k].ctypes.data, out.ctypes.data, sc.ctypes.data)
+                    return call
                 return for_thread
             cps = aggregate(mk(L), a.threads, a.seconds)
             row["gpu_decompress_threads"] = a.threads
@@ -128,9 +159,10 @@ def main():
                 row["ref_decompress_agg_GiBps"] = round(cps * n / 2**30, 3)
         rows.append(row)
         print(json.dumps(row), flush=True)
-    res = {"what": "median per-call latency, one call at a time (ctypes on both sides), text values; "
-                   "agg_*: aggregate qlz_decompress rate of --threads concurrent callers",
-           "calls_per_point": a.calls, "rows": rows,
+    res = {"what": "median per-call latency, one call at a time (ctypes on both sides), text values, each call "
+                   "on the next of --values distinct values; agg_*: aggregate qlz_decompress rate of --threads "
+                   "concurrent Python callers (tools/mt_single.c gives the pthread figure)",
+           "calls_per_point": a.calls, "values_per_size": a.values, "rows": rows,
            "reference": "oracle/_ref (quicklz.c, crc32.go preamble; gcc -O2)" if ref else None}
     if a.out:
         with open(a.out, "w") as f:
