@@ -24,13 +24,17 @@
 namespace qlzx {
 
 // ------------------------------------------------------------------------------- K1 ----
+// S: ring depth in rounds (kRingWaveS); chunks of few waves take S = 8 (qlzx_decode_wave.hip).
+constexpr uint32_t kDeepRingWaves = 2560;  // 2.5 waves per SIMD: 10 one-wave workgroups of 16 KiB per CU
+template <uint32_t S>
 __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
                                                      int32_t *status, uint32_t first, uint32_t count, BlkInfo *info,
                                                      GroupRec *recs, uint32_t gmax, const uint32_t *order,
                                                      uint32_t max_dsize) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG / 64) * kRingWave];
+    static_assert(S == 4 || S == 8, "ring depth");
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG / 64) * kRingWaveS<S>];
     const uint32_t lane = threadIdx.x & 63;
-    uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWave;
+    uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWaveS<S>;
     const uint32_t lin = blockIdx.x * kParseWG + threadIdx.x;
     const bool inrange = lin < count;
     const uint32_t i = inrange ? (order ? order[lin] : first + lin) : first;
@@ -65,13 +69,12 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
 
     PROF_DECL
     const uint8_t *dummy = (const uint8_t *)(((uintptr_t)b.src) & ~(uintptr_t)15);
-    ring_issue(ring, gbase, dummy, 0, last16, stream);
-    ring_issue(ring, gbase, dummy, 1, last16, stream && last_round >= 1);
-    ring_issue(ring, gbase, dummy, 2, last16, stream && last_round >= 2);
+#pragma unroll
+    for (uint32_t r0 = 0; r0 + 1 < S; r0++) ring_issue<S>(ring, gbase, dummy, r0, last16, stream && r0 <= last_round);
     for (uint32_t r = 0;; r++) {
         if (__ballot(stream && r <= last_round) == 0) break;
         PROF_MARK(0);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kPieces) : "memory");  // all but the newest two rounds
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 2) * kPieces) : "memory");  // all but the newest S - 2 rounds
         PROF_MARK(1);
         const bool act = stream && r <= last_round;
         const uint32_t lim = (r + 1) * kRoundBytes - shift;  // stream bytes below lim have landed
@@ -90,7 +93,7 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
             const uint32_t need = gb ? 4u : 1u;
             const bool landed = q + need <= lim;
             const bool stepping = go & !end & ((gb | hasm) ? landed : true);
-            const uint32_t w = ring_rd32(ring, q + shift, lane);
+            const uint32_t w = ring_rd32<S>(ring, q + shift, lane);
             const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
             const uint32_t e = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);  // token bytes - 1
             // a second match right after the first when its first byte is already in w
@@ -123,7 +126,7 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
         }
         PROF_MARK(3);
         if (done_parse) stream = false;
-        ring_issue(ring, gbase, dummy, r + 3, last16, stream && r + 3 <= last_round);
+        ring_issue<S>(ring, gbase, dummy, r + S - 1, last16, stream && r + S - 1 <= last_round);
     }
     PROF_MARK(4);
     if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, cwg, ra, rb};

@@ -52,8 +52,12 @@ __host__ __device__ inline uint32_t first_chunk_blocks(uint32_t max_dsize) {
 }
 constexpr uint32_t kRoundBytes = 32;  // bytes DMA'd per lane per round (16 B pieces; 32 measured best)
 constexpr uint32_t kPieces = kRoundBytes / 16;
-constexpr uint32_t kRingSlots = 4;            // rounds resident per lane: r-1..r (read), r+1..r+2 (landing)
-constexpr uint32_t kRingWave = kRingSlots * kRoundBytes * 64;  // 16 KiB per wave at 64-B rounds
+// Ring depth S (K1 template): S rounds resident per lane, r-1..r being read and r+1..r+S-2
+// landing.  S = 4 (8 KiB per wave) when the chunk has enough waves to hide the DMA latency by
+// occupancy (c2: 4 waves per SIMD); S = 8 (16 KiB, six rounds in flight) for chunks of few waves,
+// where a lane walking a long stream would otherwise wait about one latency per two rounds.
+template <uint32_t S>
+constexpr uint32_t kRingWaveS = S * kRoundBytes * 64;
 __host__ __device__ inline uint32_t groups_max(uint32_t max_dsize) { return max_dsize / 31u + 2u; }
 
 inline size_t rec_bytes_max(uint32_t md) { return (size_t)groups_max(md) * sizeof(GroupRec); }
@@ -163,30 +167,33 @@ __device__ __forceinline__ int classify_block(const uint8_t *src, uint32_t len, 
     return QLZX_OK;
 }
 
-// Ring layout per wave: [slot][piece 0..3][lane][16 B]; stream byte p of a lane
-// (q = p + shift, shift = src & 15) lives in round q/64, slot (q/64) % 4,
-// piece (q/16) % 4, byte q % 16 -- i.e. at ((q/16) % 16) * 1 KiB + lane * 16 + q % 16.
+// Ring layout per wave: [slot][piece][lane][16 B]; stream byte p of a lane (q = p + shift,
+// shift = src & 15) lives in round q / kRoundBytes, slot round % S, piece (q / 16) % kPieces,
+// byte q % 16 -- i.e. at ((q / 16) % (kPieces S)) * 1 KiB + lane * 16 + q % 16.
+template <uint32_t S>
 __device__ __forceinline__ uint32_t ring_off(uint32_t q, uint32_t lane) {
-    return (((q >> 4) & (kPieces * kRingSlots - 1)) << 10) | (lane << 4) | (q & 15u);
+    return (((q >> 4) & (kPieces * S - 1)) << 10) | (lane << 4) | (q & 15u);
 }
+template <uint32_t S>
 __device__ __forceinline__ uint32_t ring_rd32(const uint8_t *ring, uint32_t q, uint32_t lane) {
     const uint32_t qa = q & ~3u;
-    const uint32_t lo = *(const uint32_t *)(ring + ring_off(qa, lane));
-    const uint32_t hi = *(const uint32_t *)(ring + ring_off(qa + 4, lane));
+    const uint32_t lo = *(const uint32_t *)(ring + ring_off<S>(qa, lane));
+    const uint32_t hi = *(const uint32_t *)(ring + ring_off<S>(qa + 4, lane));
     return __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
 }
 
-// DMA round r (q in [64r, 64r+64)) of every lane into its ring slot.  All
-// lanes always issue exactly 4 DMAs per round (inactive lanes fetch a dummy
-// chunk of the source buffer's first bytes into their own, unused, slot) so
-// that "s_waitcnt vmcnt(8)" means exactly "every round but the newest two landed".
+// DMA round r of every lane into its ring slot.  All lanes always issue exactly kPieces DMAs
+// per round (inactive lanes fetch a dummy piece of the source buffer's first bytes into their
+// own, unused, slot) so that "s_waitcnt vmcnt((S - 2) kPieces)" means exactly "every round but
+// the newest S - 2 landed".
+template <uint32_t S>
 __device__ __forceinline__ void ring_issue(uint8_t *ring_wave, const uint8_t *gbase, const uint8_t *dummy,
                                            uint32_t r, uint32_t last16, bool active) {
 #pragma unroll
     for (uint32_t j = 0; j < kPieces; j++) {
         const uint32_t c16 = r * kPieces + j;
         const uint8_t *g = (active && c16 <= last16) ? gbase + (size_t)c16 * 16 : dummy;
-        dma16(g, lds_addr(ring_wave + ((r & (kRingSlots - 1)) * kPieces + j) * 1024));
+        dma16(g, lds_addr(ring_wave + ((r & (S - 1)) * kPieces + j) * 1024));
     }
 }
 
@@ -288,20 +295,22 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     // per host thread (the batch API is re-entrant like the reference) and per device: the
     // side stream and events are created on the device that owns `s`
     struct Side {  // destroyed with the thread (Go runs cgo calls on many OS threads)
-        hipStream_t st = nullptr;
-        hipEvent_t k1[2] = {}, k2[2] = {};
+        hipStream_t st = nullptr, st2 = nullptr;
+        hipEvent_t k1[2] = {}, k2[2] = {}, order = nullptr;
         ~Side() {
             if (!st || g_hip_down.load()) return;
             for (int j = 0; j < 2; j++) {
                 if (k1[j]) (void)hipEventDestroy(k1[j]);
                 if (k2[j]) (void)hipEventDestroy(k2[j]);
             }
+            if (order) (void)hipEventDestroy(order);
+            if (st2) (void)hipStreamDestroy(st2);
             (void)hipStreamDestroy(st);
         }
     };
     thread_local Side sides[kMaxDevices];
-    hipStream_t side = nullptr;
-    hipEvent_t *ev_k1 = nullptr, *ev_k2 = nullptr;
+    hipStream_t side = nullptr, side2 = nullptr;
+    hipEvent_t *ev_k1 = nullptr, *ev_k2 = nullptr, ev_order = nullptr;
     if (overlap) {
         int dev = 0, cur = 0;
         if (s) {
@@ -318,6 +327,8 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
             (void)hipGetDevice(&cur);
             if (cur != dev) (void)hipSetDevice(dev);
             hipError_t e = hipStreamCreateWithFlags(&sd.st, hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&sd.st2, hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&sd.order, hipEventDisableTiming);
             for (int j = 0; j < 2 && e == hipSuccess; j++) {
                 e = hipEventCreateWithFlags(&sd.k1[j], hipEventDisableTiming);
                 if (e == hipSuccess) e = hipEventCreateWithFlags(&sd.k2[j], hipEventDisableTiming);
@@ -326,11 +337,20 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
             if (e != hipSuccess) return (int)e;
         }
         side = sd.st;
+        side2 = sd.st2;
         ev_k1 = sd.k1;
         ev_k2 = sd.k2;
+        ev_order = sd.order;
     }
     const bool crc = crc_state || crc_expect || crc_out;
+    // Mixed block sizes (chunks of 131 072, smallest blocks first): K1 of the odd chunks runs on a
+    // second side stream, so K1 of chunk c+1 waits only for its workspace half (K2 of chunk c-1),
+    // not for K1 of chunk c.  The last chunk holds the longest streams, and its K1 (one lane
+    // per block, latency-bound) then starts with the first K1 instead of after it.  Uniform
+    // 16 KiB chunks keep one side stream: there two concurrent K1s only slow each other down.
+    const bool split_k1 = overlap && max_dsize > 16384;
     if (overlap) (void)hipEventRecord(ev_k2[1], s), (void)hipStreamWaitEvent(side, ev_k2[1], 0);
+    if (split_k1) (void)hipStreamWaitEvent(side2, ev_k2[1], 0);
     if (sort) {  // block order of the whole call, ahead of the first K1 (workspace half 0)
         hipStream_t s1 = overlap ? side : s;
         uint32_t *aux = (uint32_t *)((uint8_t *)ws + o_aux);
@@ -339,6 +359,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         hipLaunchKernelGGL(k_order_count, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, aux);
         hipLaunchKernelGGL(k_order_scatter, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, aux,
                            (uint32_t *)((uint8_t *)ws + o_list));
+        if (split_k1) (void)hipEventRecord(ev_order, side), (void)hipStreamWaitEvent(side2, ev_order, 0);
     }
     uint32_t c = 0;
     for (uint32_t first = 0, cnt = 0; first < b.n; first += cnt, c++) {
@@ -348,13 +369,18 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         BlkInfo *info = (BlkInfo *)w;
         GroupRec *recs = (GroupRec *)(w + o_rec);
         uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
-        hipStream_t s1 = overlap ? side : s;
-        if (overlap && c >= 2) (void)hipStreamWaitEvent(side, ev_k2[c & 1], 0);  // K2(c-2) freed this half
-        hipLaunchKernelGGL(k_dec_parse4,
-                           dim3((cnt + kParseWG - 1) / kParseWG),
-                           dim3(kParseWG), 0, s1, b, dst_cap, dsize, status, first, cnt, info, recs, gmax, order,
-                           max_dsize);
-        if (overlap) (void)hipEventRecord(ev_k1[c & 1], side), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
+        hipStream_t s1 = overlap ? (split_k1 && (c & 1) ? side2 : side) : s;
+        if (overlap && c >= 2) (void)hipStreamWaitEvent(s1, ev_k2[c & 1], 0);  // K2(c-2) freed this half
+        // a chunk of at most 2.5 waves per SIMD gets the deep ring at no cost in occupancy (16 KiB
+        // of LDS per one-wave workgroup: 10 per CU)
+        const uint32_t nwaves = (cnt + kParseWG - 1) / kParseWG;
+        if (nwaves <= kDeepRingWaves)
+            hipLaunchKernelGGL(k_dec_parse4<8>, dim3(nwaves), dim3(kParseWG), 0, s1, b, dst_cap, dsize, status, first,
+                               cnt, info, recs, gmax, order, max_dsize);
+        else
+            hipLaunchKernelGGL(k_dec_parse4<4>, dim3(nwaves), dim3(kParseWG), 0, s1, b, dst_cap, dsize, status, first,
+                               cnt, info, recs, gmax, order, max_dsize);
+        if (overlap) (void)hipEventRecord(ev_k1[c & 1], s1), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
         // one kernel for every block size: the LDS window slides over longer blocks
         if (crc)
             hipLaunchKernelGGL(k_dec_chunk4<true>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,

@@ -5,7 +5,7 @@ to the end of the run, per pass (tools only).
 usage: python tools/traffic_call.py gpurun_out/TAG FIRST_KERNEL CALL_BYTES OUT.json
 Host<->device copies (__amd_rocclr_copyBuffer: the end-to-end leg's pinned D2H) are not part of a
 device-resident call and are left out.
-  c4: FIRST_KERNEL k_rp_slots (replay index), CALL_BYTES = chunk bytes of that replay
+  c4: FIRST_KERNEL k_rp_scan (replay index), CALL_BYTES = chunk bytes of that replay
   c5: FIRST_KERNEL k_order_count (batch decompress), CALL_BYTES = decompressed bytes of the round
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch; FETCH_SIZE is doubled per MI355X_MICROARCH.md (HBM
 section: gfx950 counts half the bytes of 16-B-per-lane streaming reads), WRITE_SIZE is taken as is.
