@@ -24,8 +24,7 @@
 namespace qlzx {
 
 // ------------------------------------------------------------------------------- K1 ----
-// S: ring depth in rounds (kRingWaveS); chunks of few waves take S = 8 (qlzx_decode_wave.hip).
-constexpr uint32_t kDeepRingWaves = 2560;  // 2.5 waves per SIMD: 10 one-wave workgroups of 16 KiB per CU
+// S: ring depth in rounds (kRingWaveS, qlzx_decode_wave.hip)
 template <uint32_t S>
 __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
                                                      int32_t *status, uint32_t first, uint32_t count, BlkInfo *info,

@@ -53,9 +53,10 @@ __host__ __device__ inline uint32_t first_chunk_blocks(uint32_t max_dsize) {
 constexpr uint32_t kRoundBytes = 32;  // bytes DMA'd per lane per round (16 B pieces; 32 measured best)
 constexpr uint32_t kPieces = kRoundBytes / 16;
 // Ring depth S (K1 template): S rounds resident per lane, r-1..r being read and r+1..r+S-2
-// landing.  S = 4 (8 KiB per wave) when the chunk has enough waves to hide the DMA latency by
-// occupancy (c2: 4 waves per SIMD); S = 8 (16 KiB, six rounds in flight) for chunks of few waves,
-// where a lane walking a long stream would otherwise wait about one latency per two rounds.
+// landing.  kRingSlots = 4 (8 KiB per wave).  An 8-round ring (16 KiB, six rounds in flight)
+// for chunks of few waves gained 0.16 ms on c4's 4.4 ms chunk of long streams (their lanes
+// are bound by the serial step chain, not by the DMA latency) and was dropped in round 5.
+constexpr uint32_t kRingSlots = 4;
 template <uint32_t S>
 constexpr uint32_t kRingWaveS = S * kRoundBytes * 64;
 __host__ __device__ inline uint32_t groups_max(uint32_t max_dsize) { return max_dsize / 31u + 2u; }
@@ -343,12 +344,13 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         ev_order = sd.order;
     }
     const bool crc = crc_state || crc_expect || crc_out;
-    // Mixed block sizes (chunks of 131 072, smallest blocks first): K1 of the odd chunks runs on a
-    // second side stream, so K1 of chunk c+1 waits only for its workspace half (K2 of chunk c-1),
-    // not for K1 of chunk c.  The last chunk holds the longest streams, and its K1 (one lane
-    // per block, latency-bound) then starts with the first K1 instead of after it.  Uniform
-    // 16 KiB chunks keep one side stream: there two concurrent K1s only slow each other down.
-    const bool split_k1 = overlap && max_dsize > 16384;
+    // A call of two chunks of mixed block sizes (smallest blocks first): K1 of the second chunk
+    // runs on a second side stream, so it starts with the first K1 instead of after it.  It holds
+    // the longest streams, and its K1 (one lane per block, latency-bound) was the critical path
+    // (c4: 15.3 -> 11.7 ms per 4000 MiB chunk with k_rp_scan).  Calls of more chunks (c5's
+    // rounds: 560 vs 620 GiB/s) and uniform 16 KiB chunks keep one side stream: there concurrent
+    // K1s only compete with the K2s.
+    const bool split_k1 = overlap && max_dsize > 16384 && b.n <= chunk0 + chunk;  // two chunks (c4's calls)
     if (overlap) (void)hipEventRecord(ev_k2[1], s), (void)hipStreamWaitEvent(side, ev_k2[1], 0);
     if (split_k1) (void)hipStreamWaitEvent(side2, ev_k2[1], 0);
     if (sort) {  // block order of the whole call, ahead of the first K1 (workspace half 0)
@@ -371,15 +373,8 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
         hipStream_t s1 = overlap ? (split_k1 && (c & 1) ? side2 : side) : s;
         if (overlap && c >= 2) (void)hipStreamWaitEvent(s1, ev_k2[c & 1], 0);  // K2(c-2) freed this half
-        // a chunk of at most 2.5 waves per SIMD gets the deep ring at no cost in occupancy (16 KiB
-        // of LDS per one-wave workgroup: 10 per CU)
-        const uint32_t nwaves = (cnt + kParseWG - 1) / kParseWG;
-        if (nwaves <= kDeepRingWaves)
-            hipLaunchKernelGGL(k_dec_parse4<8>, dim3(nwaves), dim3(kParseWG), 0, s1, b, dst_cap, dsize, status, first,
-                               cnt, info, recs, gmax, order, max_dsize);
-        else
-            hipLaunchKernelGGL(k_dec_parse4<4>, dim3(nwaves), dim3(kParseWG), 0, s1, b, dst_cap, dsize, status, first,
-                               cnt, info, recs, gmax, order, max_dsize);
+        hipLaunchKernelGGL(k_dec_parse4<kRingSlots>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b,
+                           dst_cap, dsize, status, first, cnt, info, recs, gmax, order, max_dsize);
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], s1), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
         // one kernel for every block size: the LDS window slides over longer blocks
         if (crc)
