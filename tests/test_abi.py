@@ -20,10 +20,16 @@ def test_library_builds_and_exports_header_symbols():
     assert set(names) <= exported
 
 
-def test_gfx950_code_object_present():
-    # the fat binary carries an offload bundle entry for the gfx950 code object
-    blob = open(_lib.LIB_PATH, "rb").read()
-    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+def test_gfx950_code_object_present(tmp_path):
+    # the fat binary (.hip_fatbin, a zstd-compressed offload bundle since round 5) carries a
+    # gfx950 code object: list the bundle's entries with the ROCm LLVM tools
+    bin_dir = "/opt/rocm/lib/llvm/bin"
+    fb = tmp_path / "fatbin.bin"
+    subprocess.run([f"{bin_dir}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", _lib.LIB_PATH,
+                    str(tmp_path / "host.o")], check=True)
+    out = subprocess.run([f"{bin_dir}/clang-offload-bundler", "--list", "--type=o", f"--input={fb}"],
+                         capture_output=True, text=True, check=True).stdout
+    assert "hipv4-amdgcn-amd-amdhsa--gfx950" in out.split()
 
 
 def test_settings_match_reference(golden):
