@@ -1,11 +1,12 @@
-// qlzx_decode_v4.hip -- the batch decoder pair (dsize <= QLZX_FAST_MAX_DSIZE), round 4:
+// qlzx_decode_v4.hip -- the batch decoder pair (dsize <= QLZX_FAST_MAX_DSIZE):
 //
-// K1 k_dec_parse4  one LANE per block: the serial control-word chain of quicklz.c:513-671,
-//     one item STEP at a time (a literal run and the match that ends it, or a control word),
-//     reading only control words and the first byte of each match token.  The remaining
-//     control bits are kept with their sentinel (cwr; 1 = group exhausted), so the item index
-//     is clz(cwr) and a literal run is ctz(cwr): no per-item counters, no multi-match step.
-//     Emits one GroupRec {ip, cw, a, b} per control word (a, b: bit-planes of token bytes - 1).
+// K1 k_dec_parse6 (round 5)  one LANE per block: the serial control-word chain of
+//     quicklz.c:513-671, one item STEP at a time (a literal run and the match that ends it, or a
+//     control word), reading only control words and the first byte of each match token from a
+//     per-lane LDS ring the lane refills itself.  The remaining control bits are kept with their
+//     sentinel (cwr; 1 = group exhausted), so the item index is clz(cwr) and a literal run is
+//     ctz(cwr): no per-item counters.  Emits one GroupRec {ip, cw, a, b} per control word (a, b:
+//     bit-planes of token bytes - 1).
 //
 // K2 k_dec_chunk4  one WAVE per block, 64 items per batch and 256 output bytes per chunk:
 //     * ITEM PHASE: token position from the GroupRec, branch-free token decode, DPP scan of the
@@ -24,13 +25,20 @@
 namespace qlzx {
 
 // ------------------------------------------------------------------------------- K1 ----
-// S: ring depth in rounds (kRingWaveS, qlzx_decode_wave.hip)
-template <uint32_t S>
-__global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
+// K1 k_dec_parse6 (round 5): one LANE per block walks the serial control-word chain.  Each lane
+// refills its own LDS ring: an iteration writes the rounds (32 B) loaded in the previous
+// iteration into the lane's slots, issues plain global loads for up to two more rounds the ring
+// has room for, then takes at most `kmax` steps.  Round 4's k_dec_parse4 moved every lane of a
+// wave through the same round (one LDS-DMA per round into a wave-uniform slot) and looped until
+// the lane with the most steps in that round was done: the wave paid max-over-lanes steps per
+// round.  Here lanes drift apart in stream position and the wave pays kmax steps per iteration.
+// c2 25.1-25.3 -> 24.7-24.9 ms at kmax 16; c4 346 -> 377 GiB/s at kmax 10
+// (tools/gpu_r5lr3.sh, profiles/r05_k1_lane_ring_ab.txt).
+__global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
                                                      int32_t *status, uint32_t first, uint32_t count, BlkInfo *info,
                                                      GroupRec *recs, uint32_t gmax, const uint32_t *order,
-                                                     uint32_t max_dsize) {
-    static_assert(S == 4 || S == 8, "ring depth");
+                                                     uint32_t max_dsize, uint32_t kmax) {
+    constexpr uint32_t S = kRingSlots;
     __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG / 64) * kRingWaveS<S>];
     const uint32_t lane = threadIdx.x & 63;
     uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWaveS<S>;
@@ -44,9 +52,7 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
     if (inrange) {
         len = b.src_len[i];
         st = classify_block(src, len, dst_cap ? dst_cap[i] : 0xffffffffu, max_dsize, kind, csize, dsize, hdr);
-        // a compressed stream of dsize 0 decodes to nothing: the oracle's loop never runs and C5
-        // accepts csize == hdr or the 9-byte core minimum (oracle/qlz_oracle.c:197,228)
-        if (st == QLZX_OK && kind == kBlkCompressed && dsize == 0) {
+        if (st == QLZX_OK && kind == kBlkCompressed && dsize == 0) {  // oracle/qlz_oracle.c:197,228
             st = (csize == hdr || csize == hdr + 9) ? QLZX_OK : QLZX_E_CORRUPT;
             kind = kBlkSkip;
         }
@@ -56,46 +62,71 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
     const uint32_t shift = (uint32_t)(a0 & 15);
     const uint32_t span = (st == QLZX_OK && kind == kBlkCompressed) ? csize : 0;
     const uint32_t last16 = span ? (span + shift - 1) >> 4 : 0;
-    const uint32_t last_round = span ? (span + shift - 1) / kRoundBytes : 0;
-    bool stream = inrange && span > 0;
-    const bool parsing = stream;
+    const uint32_t nrounds = span ? (span + shift - 1) / kRoundBytes + 1 : 0;
+    const bool parsing = inrange && span > 0;
 
-    // parse state: ip = next stream byte; cwr = control bits not consumed yet, sentinel
-    // included (1: the group is exhausted, the next step reads a control word)
     uint32_t ip = hdr, g = 0, cwr = 1, cwg = 0, ra = 0, rb = 0, rec_ip = 0;
     GroupRec *myrec = recs + (size_t)(inrange ? lin : 0) * gmax;
     bool done_parse = !parsing;
 
-    PROF_DECL
-    const uint8_t *dummy = (const uint8_t *)(((uintptr_t)b.src) & ~(uintptr_t)15);
-#pragma unroll
-    for (uint32_t r0 = 0; r0 + 1 < S; r0++) ring_issue<S>(ring, gbase, dummy, r0, last16, stream && r0 <= last_round);
-    for (uint32_t r = 0;; r++) {
-        if (__ballot(stream && r <= last_round) == 0) break;
-        PROF_MARK(0);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 2) * kPieces) : "memory");  // all but the newest S - 2 rounds
-        PROF_MARK(1);
-        const bool act = stream && r <= last_round;
-        const uint32_t lim = (r + 1) * kRoundBytes - shift;  // stream bytes below lim have landed
-        if (act && !done_parse) {
-        bool go = true;
-        while (go) {  // per-lane loop: the exec mask carries go (no cross-lane op in the step)
-            PROF_COUNT(5, 1);
+    // ring bookkeeping: rounds [0, rl) are in the lane's slots (round r in slot r % S), rounds
+    // [rl, ri) are loaded into registers and go to the slots at the next iteration
+    uint32_t rl = 0, ri = 0;
+    // accept up to two rounds: a round r may overwrite round r - S only once the lane reads no
+    // byte below round r - S + 1 (ring_rd32 reads the aligned dwords at and after its position)
+    auto accept = [&]() __attribute__((always_inline)) -> uint32_t {
+        const uint32_t cap = ((ip + shift) & ~3u) / kRoundBytes + S - 1;  // last round the ring can take
+        uint32_t n = 0;
+        if (!done_parse && ri < nrounds && ri <= cap) n = (ri + 1 < nrounds && ri + 1 <= cap) ? 2u : 1u;
+        return n;
+    };
+    // the two rounds from ri on (16-B pieces 2 ri .. 2 ri + 3), clamped into the stream; a lane
+    // taking fewer rounds loads the stream's first piece instead (cached, never written)
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(1))) u4v g_u4;
+    const uintptr_t gaddr = (uintptr_t)gbase;  // integer -> global pointer: global_load, not flat
+#define K1_LOAD(n, v0, v1, v2, v3)                                                                \
+    do {                                                                                          \
+        const uint32_t c16 = ri * kPieces;                                                        \
+        v0 = *(g_u4 *)(gaddr + (size_t)((n) >= 1 ? min(c16, last16) : 0u) * 16);                  \
+        v1 = *(g_u4 *)(gaddr + (size_t)((n) >= 1 ? min(c16 + 1, last16) : 0u) * 16);              \
+        v2 = *(g_u4 *)(gaddr + (size_t)((n) >= 2 ? min(c16 + 2, last16) : 0u) * 16);              \
+        v3 = *(g_u4 *)(gaddr + (size_t)((n) >= 2 ? min(c16 + 3, last16) : 0u) * 16);              \
+        ri += (n);                                                                                \
+    } while (0)
+    // rounds rl .. rl + n - 1 into their slots
+#define K1_STORE(n, v0, v1, v2, v3)                                                               \
+    do {                                                                                          \
+        /* an unconditional use: the loads land here in every lane, so no later reuse of their   \
+           registers waits on a vmcnt that also counts the newer loads */                         \
+        asm volatile("" ::"v"(v0.x), "v"(v0.y), "v"(v0.z), "v"(v0.w), "v"(v1.x), "v"(v1.y),        \
+                     "v"(v1.z), "v"(v1.w), "v"(v2.x), "v"(v2.y), "v"(v2.z), "v"(v2.w), "v"(v3.x),  \
+                     "v"(v3.y), "v"(v3.z), "v"(v3.w));                                             \
+        uint8_t *sl0 = ring + (((rl & (S - 1)) * kPieces) << 10) + lane * 16;                     \
+        uint8_t *sl1 = ring + ((((rl + 1) & (S - 1)) * kPieces) << 10) + lane * 16;               \
+        if ((n) >= 1) *(u4v *)sl0 = v0, *(u4v *)(sl0 + 1024) = v1;                                \
+        if ((n) >= 2) *(u4v *)sl1 = v2, *(u4v *)(sl1 + 1024) = v3;                                \
+        rl += (n);                                                                                \
+    } while (0)
+    auto steps = [&]() __attribute__((always_inline)) {
+        const uint32_t lim = rl * kRoundBytes - shift;  // stream bytes below lim are in the ring
+        bool go = !done_parse;
+        uint32_t k = 0;
+        while (go) {  // per-lane loop, at most kmax steps
             const bool gb = cwr == 1;
             const uint32_t rem = csize - ip;
-            uint32_t run = __builtin_ctz(cwr);  // literals before the next match (or the sentinel)
+            uint32_t run = __builtin_ctz(cwr);
             run = run < rem ? run : rem;
-            const uint32_t q = ip + run;        // control word (gb) or the match token
+            const uint32_t q = ip + run;
             const uint32_t rest = cwr >> run;
             const bool hasm = !gb & (rest != 1u) & ((rest & 1u) != 0) & (q < csize);
             const bool end = ip + (gb ? 4u : 1u) > csize;
             const uint32_t need = gb ? 4u : 1u;
             const bool landed = q + need <= lim;
-            const bool stepping = go & !end & ((gb | hasm) ? landed : true);
+            const bool stepping = !end & ((gb | hasm) ? landed : true);
             const uint32_t w = ring_rd32<S>(ring, q + shift, lane);
             const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
-            const uint32_t e = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);  // token bytes - 1
-            // a second match right after the first when its first byte is already in w
+            const uint32_t e = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);
             const uint32_t q2 = q + e + 1, rest2 = rest >> 1;
             const bool hasm2 = hasm & (e < 3u) & ((rest2 & 1u) != 0) & (rest2 != 1u) & (q2 < csize) & (q2 + 1 <= lim);
             const uint32_t w2 = w >> (8 * ((e + 1) & 3u));
@@ -103,10 +134,17 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
             const uint32_t e2 = hasm2 ? __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4) : 0u;
             const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) | (hasm & (q2 > csize)) |
                                          (hasm2 & (q2 + e2 + 1 > csize)));
-            if (stepping & gb & (g > 0)) myrec[g - 1] = GroupRec{rec_ip, cwg, ra, rb};
+            // the record store is invisible to the compiler's vmcnt bookkeeping: counted, it made
+            // every wait before the step loop a vmcnt(0), i.e. a wait for the loads just issued
+            // (an unseen store only makes the compiler's later vmcnt(N) waits stricter)
+            if (stepping & gb & (g > 0)) {
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 rec = {rec_ip, cwg, ra, rb};
+                asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(myrec + (g - 1)), "v"(rec) : "memory");
+            }
             st = bad ? QLZX_E_CORRUPT : st;
             const bool adv = stepping & !bad;
-            const uint32_t kb = hasm ? 1u << (__builtin_clz(cwr) + run) : 0u;  // item index clz(cwr) + run
+            const uint32_t kb = hasm ? 1u << (__builtin_clz(cwr) + run) : 0u;
             const uint32_t kb2 = hasm2 ? kb << 1 : 0u;
             const uint32_t nip = gb ? ip + 4 : q + (hasm ? e + 1 : 0u) + (hasm2 ? e2 + 1 : 0u);
             const uint32_t ncwr = gb ? w : (rest >> (hasm ? (hasm2 ? 2 : 1) : 0));
@@ -119,17 +157,41 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
             cwr = adv ? ncwr : cwr;
             ra = adv ? nra : ra;
             rb = adv ? nrb : rb;
-            done_parse = done_parse | (go & (end | bad));
-            go = adv;
+            done_parse = done_parse | end | bad;
+            go = adv && ++k < kmax;
         }
-        }
-        PROF_MARK(3);
-        if (done_parse) stream = false;
-        ring_issue<S>(ring, gbase, dummy, r + S - 1, last16, stream && r + S - 1 <= last_round);
+    };
+
+    u4v pa0, pa1, pa2, pa3, pb0, pb1, pb2, pb3;
+    uint32_t na = accept();
+    K1_LOAD(na, pa0, pa1, pa2, pa3);
+    uint32_t nb = 0;
+    // Every iteration a lane either steps or lands a round, so csize + nrounds iterations finish
+    // any stream; past that bound a lane stops as corrupt (a guard: the loop always ends).
+    const uint32_t trip_cap = span + nrounds + 8;
+    uint32_t trips = 0;
+    auto guard = [&]() __attribute__((always_inline)) {
+        trips++;
+        if (!done_parse && trips > trip_cap) done_parse = true, st = QLZX_E_CORRUPT;
+    };
+    // two iterations per loop trip: register sets va / vb alternate, no copies of loaded data
+    for (;;) {
+        K1_STORE(na, pa0, pa1, pa2, pa3);
+        nb = accept();
+        K1_LOAD(nb, pb0, pb1, pb2, pb3);
+        steps();
+        guard();
+        if (__ballot(!done_parse) == 0) break;
+        K1_STORE(nb, pb0, pb1, pb2, pb3);
+        na = accept();
+        K1_LOAD(na, pa0, pa1, pa2, pa3);
+        steps();
+        guard();
+        if (__ballot(!done_parse) == 0) break;
     }
-    PROF_MARK(4);
+#undef K1_LOAD
+#undef K1_STORE
     if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, cwg, ra, rb};
-    PROF_FLUSH(0);
     vm_sync();
     if (!inrange) return;
     if (st == QLZX_OK && kind == kBlkCompressed && (!done_parse || g == 0)) st = QLZX_E_CORRUPT;
@@ -140,8 +202,8 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse4(qlzx_blocks b, const ui
         if (dsize_out && st != kPending) dsize_out[i] = 0;
     } else if (kind == kBlkCompressed) {
         bi.ngroups = g;
-        bi.nitems = (g - 1) * 31 + __builtin_clz(cwr);  // items consumed in the last group
-    } else if (kind == kBlkSkip) {  // dsize-0 compressed stream accepted above
+        bi.nitems = (g - 1) * 31 + __builtin_clz(cwr);
+    } else if (kind == kBlkSkip) {
         status[i] = QLZX_OK;
         if (dsize_out) dsize_out[i] = 0;
     }

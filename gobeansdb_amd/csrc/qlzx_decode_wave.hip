@@ -1,12 +1,12 @@
 // qlzx_decode_wave.hip -- fast batched level-3 decoder for blocks with
 // dsize <= QLZX_FAST_MAX_DSIZE (the 4-64 KiB values of the BASELINE configs).
 //
-// Kernels per chunk of blocks: K1 k_dec_parse4 (one LANE per block: the serial
+// Kernels per chunk of blocks: K1 k_dec_parse6 (one LANE per block: the serial
 // control-word chain of quicklz.c:513-671, one 16-B GroupRec per control word) and K2
 // k_dec_chunk4 (one WAVE per block: items 64 at a time, output 256 bytes at a time, every byte
 // gathered from the position it copies; the record CRC is verified first when asked for,
 // store/datafile.go:161-168).  Both are in qlzx_decode_v4.hip; this file holds the shared
-// types, the block order, the header checks, K1's DMA ring and the launcher.
+// types, the block order, the header checks, K1's ring layout and the launcher.
 //
 // K1 of chunk c+1 runs on a side stream beside K2 of chunk c.
 #include "qlzx_device.h"
@@ -50,12 +50,11 @@ __host__ __device__ inline uint32_t chunk_blocks(uint32_t max_dsize) {
 __host__ __device__ inline uint32_t first_chunk_blocks(uint32_t max_dsize) {
     return QLZX_FIRST_CHUNK < chunk_blocks(max_dsize) ? (uint32_t)QLZX_FIRST_CHUNK : chunk_blocks(max_dsize);
 }
-constexpr uint32_t kRoundBytes = 32;  // bytes DMA'd per lane per round (16 B pieces; 32 measured best)
+constexpr uint32_t kRoundBytes = 32;  // bytes of a lane's stream per ring slot (16-B pieces)
 constexpr uint32_t kPieces = kRoundBytes / 16;
-// Ring depth S (K1 template): S rounds resident per lane, r-1..r being read and r+1..r+S-2
-// landing.  kRingSlots = 4 (8 KiB per wave).  An 8-round ring (16 KiB, six rounds in flight)
-// for chunks of few waves gained 0.16 ms on c4's 4.4 ms chunk of long streams (their lanes
-// are bound by the serial step chain, not by the DMA latency) and was dropped in round 5.
+// K1's LDS ring: kRingSlots rounds of kRoundBytes per lane (8 KiB per wave).  An 8-round ring
+// for chunks of few waves gained 0.16 ms on c4's 4.4 ms chunk of long streams (their lanes are
+// bound by the serial step chain, not by the load latency) and was dropped in round 5.
 constexpr uint32_t kRingSlots = 4;
 template <uint32_t S>
 constexpr uint32_t kRingWaveS = S * kRoundBytes * 64;
@@ -181,21 +180,6 @@ __device__ __forceinline__ uint32_t ring_rd32(const uint8_t *ring, uint32_t q, u
     const uint32_t lo = *(const uint32_t *)(ring + ring_off<S>(qa, lane));
     const uint32_t hi = *(const uint32_t *)(ring + ring_off<S>(qa + 4, lane));
     return __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
-}
-
-// DMA round r of every lane into its ring slot.  All lanes always issue exactly kPieces DMAs
-// per round (inactive lanes fetch a dummy piece of the source buffer's first bytes into their
-// own, unused, slot) so that "s_waitcnt vmcnt((S - 2) kPieces)" means exactly "every round but
-// the newest S - 2 landed".
-template <uint32_t S>
-__device__ __forceinline__ void ring_issue(uint8_t *ring_wave, const uint8_t *gbase, const uint8_t *dummy,
-                                           uint32_t r, uint32_t last16, bool active) {
-#pragma unroll
-    for (uint32_t j = 0; j < kPieces; j++) {
-        const uint32_t c16 = r * kPieces + j;
-        const uint8_t *g = (active && c16 <= last16) ? gbase + (size_t)c16 * 16 : dummy;
-        dma16(g, lds_addr(ring_wave + ((r & (S - 1)) * kPieces + j) * 1024));
-    }
 }
 
 // ------------------------------------------------------------------- K2 helpers ----
@@ -373,8 +357,10 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
         hipStream_t s1 = overlap ? (split_k1 && (c & 1) ? side2 : side) : s;
         if (overlap && c >= 2) (void)hipStreamWaitEvent(s1, ev_k2[c & 1], 0);  // K2(c-2) freed this half
-        hipLaunchKernelGGL(k_dec_parse4<kRingSlots>, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b,
-                           dst_cap, dsize, status, first, cnt, info, recs, gmax, order, max_dsize);
+        // K1's step budget per iteration: 16 for uniform 16 KiB calls, 10 for mixed sizes (c4:
+        // 377 vs 363 GiB/s; c5 580 vs 560)
+        hipLaunchKernelGGL(k_dec_parse6, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b, dst_cap, dsize,
+                           status, first, cnt, info, recs, gmax, order, max_dsize, max_dsize > 16384 ? 10u : 16u);
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], s1), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
         // one kernel for every block size: the LDS window slides over longer blocks
         if (crc)
