@@ -74,38 +74,46 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const ui
     uint32_t rl = 0, ri = 0;
     // accept up to two rounds: a round r may overwrite round r - S only once the lane reads no
     // byte below round r - S + 1 (ring_rd32 reads the aligned dwords at and after its position)
+    // rounds loaded per iteration (at most; the ring can take up to S - 1 rounds past the one
+    // being read).  Three rounds per iteration were slower at every step budget (c2 25.3-26.2 vs
+    // 24.7 ms, c5 517-543 vs 571 GiB/s: profiles/r05_k1_lane_ring_ab.txt)
+    constexpr uint32_t M = 2;
+    static_assert(M == 2 || M == 3, "rounds per iteration");
     auto accept = [&]() __attribute__((always_inline)) -> uint32_t {
         const uint32_t cap = ((ip + shift) & ~3u) / kRoundBytes + S - 1;  // last round the ring can take
         uint32_t n = 0;
-        if (!done_parse && ri < nrounds && ri <= cap) n = (ri + 1 < nrounds && ri + 1 <= cap) ? 2u : 1u;
+#pragma unroll
+        for (uint32_t k = 0; k < M; k++) n += (!done_parse && ri + k < nrounds && ri + k <= cap) ? 1u : 0u;
         return n;
     };
-    // the two rounds from ri on (16-B pieces 2 ri .. 2 ri + 3), clamped into the stream; a lane
-    // taking fewer rounds loads the stream's first piece instead (cached, never written)
+    // the M rounds from ri on (16-B pieces 2 ri ..), clamped into the stream; a lane taking fewer
+    // rounds loads the stream's first piece instead (cached, never written)
     typedef uint32_t u4v __attribute__((ext_vector_type(4)));
     typedef const __attribute__((address_space(1))) u4v g_u4;
     const uintptr_t gaddr = (uintptr_t)gbase;  // integer -> global pointer: global_load, not flat
-#define K1_LOAD(n, v0, v1, v2, v3)                                                                \
+#define K1_LD(n, k, j) (*(g_u4 *)(gaddr + (size_t)((n) > (k) ? min(ri * kPieces + 2 * (k) + (j), last16) : 0u) * 16))
+#define K1_LOAD(n, v0, v1, v2, v3, v4, v5)                                                        \
     do {                                                                                          \
-        const uint32_t c16 = ri * kPieces;                                                        \
-        v0 = *(g_u4 *)(gaddr + (size_t)((n) >= 1 ? min(c16, last16) : 0u) * 16);                  \
-        v1 = *(g_u4 *)(gaddr + (size_t)((n) >= 1 ? min(c16 + 1, last16) : 0u) * 16);              \
-        v2 = *(g_u4 *)(gaddr + (size_t)((n) >= 2 ? min(c16 + 2, last16) : 0u) * 16);              \
-        v3 = *(g_u4 *)(gaddr + (size_t)((n) >= 2 ? min(c16 + 3, last16) : 0u) * 16);              \
+        v0 = K1_LD(n, 0, 0), v1 = K1_LD(n, 0, 1), v2 = K1_LD(n, 1, 0), v3 = K1_LD(n, 1, 1);        \
+        if (M >= 3) v4 = K1_LD(n, 2, 0), v5 = K1_LD(n, 2, 1);                                     \
         ri += (n);                                                                                \
     } while (0)
     // rounds rl .. rl + n - 1 into their slots
-#define K1_STORE(n, v0, v1, v2, v3)                                                               \
+#define K1_STORE(n, v0, v1, v2, v3, v4, v5)                                                       \
     do {                                                                                          \
         /* an unconditional use: the loads land here in every lane, so no later reuse of their   \
            registers waits on a vmcnt that also counts the newer loads */                         \
         asm volatile("" ::"v"(v0.x), "v"(v0.y), "v"(v0.z), "v"(v0.w), "v"(v1.x), "v"(v1.y),        \
                      "v"(v1.z), "v"(v1.w), "v"(v2.x), "v"(v2.y), "v"(v2.z), "v"(v2.w), "v"(v3.x),  \
                      "v"(v3.y), "v"(v3.z), "v"(v3.w));                                             \
+        if (M >= 3) asm volatile("" ::"v"(v4.x), "v"(v4.y), "v"(v4.z), "v"(v4.w), "v"(v5.x),      \
+                                 "v"(v5.y), "v"(v5.z), "v"(v5.w));                                 \
         uint8_t *sl0 = ring + (((rl & (S - 1)) * kPieces) << 10) + lane * 16;                     \
         uint8_t *sl1 = ring + ((((rl + 1) & (S - 1)) * kPieces) << 10) + lane * 16;               \
+        uint8_t *sl2 = ring + ((((rl + 2) & (S - 1)) * kPieces) << 10) + lane * 16;               \
         if ((n) >= 1) *(u4v *)sl0 = v0, *(u4v *)(sl0 + 1024) = v1;                                \
         if ((n) >= 2) *(u4v *)sl1 = v2, *(u4v *)(sl1 + 1024) = v3;                                \
+        if (M >= 3 && (n) >= 3) *(u4v *)sl2 = v4, *(u4v *)(sl2 + 1024) = v5;                      \
         rl += (n);                                                                                \
     } while (0)
     auto steps = [&]() __attribute__((always_inline)) {
@@ -162,9 +170,9 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const ui
         }
     };
 
-    u4v pa0, pa1, pa2, pa3, pb0, pb1, pb2, pb3;
+    u4v pa0, pa1, pa2, pa3, pa4, pa5, pb0, pb1, pb2, pb3, pb4, pb5;
     uint32_t na = accept();
-    K1_LOAD(na, pa0, pa1, pa2, pa3);
+    K1_LOAD(na, pa0, pa1, pa2, pa3, pa4, pa5);
     uint32_t nb = 0;
     // Every iteration a lane either steps or lands a round, so csize + nrounds iterations finish
     // any stream; past that bound a lane stops as corrupt (a guard: the loop always ends).
@@ -176,19 +184,20 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const ui
     };
     // two iterations per loop trip: register sets va / vb alternate, no copies of loaded data
     for (;;) {
-        K1_STORE(na, pa0, pa1, pa2, pa3);
+        K1_STORE(na, pa0, pa1, pa2, pa3, pa4, pa5);
         nb = accept();
-        K1_LOAD(nb, pb0, pb1, pb2, pb3);
+        K1_LOAD(nb, pb0, pb1, pb2, pb3, pb4, pb5);
         steps();
         guard();
         if (__ballot(!done_parse) == 0) break;
-        K1_STORE(nb, pb0, pb1, pb2, pb3);
+        K1_STORE(nb, pb0, pb1, pb2, pb3, pb4, pb5);
         na = accept();
-        K1_LOAD(na, pa0, pa1, pa2, pa3);
+        K1_LOAD(na, pa0, pa1, pa2, pa3, pa4, pa5);
         steps();
         guard();
         if (__ballot(!done_parse) == 0) break;
     }
+#undef K1_LD
 #undef K1_LOAD
 #undef K1_STORE
     if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, cwg, ra, rb};
