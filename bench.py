@@ -83,7 +83,7 @@ def parse():
                    help="skip the \"crc\" leg (the c2 shard again with the fused CRC verify)")
     p.add_argument("--traffic-json", default=None,
                    help="PMC HBM bytes per block (tools/traffic.py output); default: the committed "
-                        "profiles/r04_c2_traffic.json for the c2 workload")
+                        "profiles/r05_c2_traffic.json for the c2 workload")
     return p.parse_args()
 
 
@@ -257,7 +257,7 @@ def main():
     achieved = (csum + dsum) / (kern_ms * 1e-3) / 1e9
     traffic = None
     if args.traffic_json is None and args.mode == "decompress" and kind == "text" and bs == 16384 and not args.crc:
-        args.traffic_json = os.path.join(ROOT, "profiles", "r04_c2_traffic.json")
+        args.traffic_json = os.path.join(ROOT, "profiles", "r05_c2_traffic.json")
     traffic_src = None
     if args.traffic_json and os.path.exists(args.traffic_json):
         # PMC-measured HBM bytes per block (tools/traffic.py) x blocks per launch: a committed
@@ -480,7 +480,7 @@ def bench_compress(args, rank, world, dev, kind, emit: bool = True):
     achieved = (n * bs + csum) / (kern_ms * 1e-3) / 1e9
     traffic = None
     traffic_src = None
-    tj = args.traffic_json or os.path.join(ROOT, "profiles", "r04_c3_traffic.json")
+    tj = args.traffic_json or os.path.join(ROOT, "profiles", "r05_c3_traffic.json")
     if os.path.exists(tj) and kind == "image" and bs == 65536:
         tpb = json.load(open(tj)).get("hbm_bytes_per_block")
         if tpb is not None:
