@@ -141,3 +141,29 @@ def test_long_candidates(cuda):
     rows, _ = _gpu(data)
     assert rows[0][0] == 4096 and rows[0][2] == b"embedded"
     _check(data)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_pieces_replay_like_the_whole_file(cuda, world):
+    """The c4 leg's split (shard.partition_data_files, cut at gap-free record starts): every
+    piece replayed on the GPU as a stream of its own gives exactly the records, sizeBroken
+    included, that the whole-file replay gives in that range; the unexpected-EOF error only at
+    the file's end."""
+    from gobeansdb_amd import replay, shard
+    rng = random.Random(31 + world)
+    data = bytearray(_random_file(rng, 70))
+    for _ in range(8):
+        p = rng.randrange(len(data))
+        data[p] = rng.getrandbits(8)
+    data = bytes(data[: len(data) - 100])
+    whole, whole_err = _gpu(data)
+    cuts = [r[0] for r in whole if r[1] == 0]
+    plan = shard.partition_data_files([(cuts, len(data))], world)
+    union = []
+    for pieces in plan:
+        for f, lo, hi in pieces:
+            rows, err = _gpu(data[lo:hi])
+            union += [(off + lo,) + tuple(rest) for off, *rest in rows]
+            assert err == (whole_err and hi == len(data))
+    assert union == whole
+    assert sum(len(p) for p in plan) >= 2
