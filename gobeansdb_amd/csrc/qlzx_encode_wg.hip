@@ -193,89 +193,6 @@ constexpr uint32_t kPrefixMinLen = kPrefixPass ? 16384 : 0xFFFFFFFFu, kPrefixRep
                    kPrefixMargin = kPrefixMarginB;
 constexpr uint32_t kParseRounds = 4;  // segment-walker rounds before the serial item walk
 
-
-// Best match of position p (quicklz.c:310-344) among its d most recent same-bucket earlier positions:
-// cand(k), k = 0 the most recent, is the list entry pos | fetch[23:12] << 16 (any value for k >= d).
-// Longest wins, ties to the larger position: scanning from the most recent, a candidate must be
-// strictly longer, and a match of the full extension limit ends the scan.  COMPACT (poorly
-// compressible blocks): a wave whose lanes all have few candidates that can match visits only those.
-template <bool COMPACT, typename CAND>
-__device__ __forceinline__ void best_of(const uint8_t *s_in, uint32_t n, uint32_t p, uint32_t self, uint32_t d,
-        CAND cand, uint32_t &best_out, uint32_t &bpos_out) {
-    const uint32_t limit = min(255u, n - 4u - p);  // quicklz.c:310
-    // First pass: bytes 3..6 of every candidate against this position's, all
-    // LDS reads independent.  A mismatch there gives the exact length; the
-    // candidates equal through byte 6 ("long") are extended afterwards, most
-    // recent first -- they beat every short one, and ties stay with the more
-    // recent (larger) position.
-    const uint32_t P3 = ld32u(s_in, p + 3);
-    uint32_t best = 0, bpos = 0, longm = 0;
-    auto first = [&](uint32_t k, uint32_t q, bool ok) {
-        const uint32_t x = ld32u(s_in, q + 3) ^ P3;
-        const uint32_t m = min(x ? 3u + ((uint32_t)__builtin_ctz(x) >> 3) : 7u, limit);
-        if (ok && !x && limit > 7u) longm |= 1u << k;
-        else if (ok && m > best) {
-            best = m;
-            bpos = q;
-        }
-    };
-    // A candidate can match when it is in the bucket (k < d) with the same
-    // fetch[23:12] (same bucket + same fetch[23:12] = same 3 bytes) and
-    // o < src - MINOFFSET (q + 3 <= p): with fhs = fetch[23:12] << 16, the word
-    // c - fhs is q when the fetch bits agree and >= 2^16 otherwise, so one
-    // subtraction and one compare against p - 3 test both (no candidate at p < 3).
-    const uint32_t fhs = self & 0xFFFF0000u, lim3 = p - 3u;
-    const uint32_t dmask = p >= 3u ? (1u << d) - 1u : 0u;
-    if constexpr (COMPACT) {
-        uint32_t okm = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 16; k++) {
-            const uint32_t c = cand(k);
-            okm |= (c - fhs <= lim3) ? 1u << k : 0u;
-        }
-        okm &= dmask;
-        if (__ballot((uint32_t)__popc(okm) > kMatchCompactMax) == 0ull) {  // wave-uniform
-            for (uint32_t t2 = okm; t2; t2 &= t2 - 1u) {  // set bits, most recent first
-                const uint32_t k = (uint32_t)__builtin_ctz(t2);
-                first(k, cand(k) & 0xFFFFu, true);
-            }
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < 16; k++) first(k, cand(k) & 0xFFFFu, (okm >> k) & 1u);
-        }
-    } else {
-        uint32_t cv[16];  // most recent first
-#pragma unroll
-        for (uint32_t k = 0; k < 16; k++) cv[k] = cand(k);
-#pragma unroll
-        for (uint32_t k = 0; k < 16; k++)
-            first(k, cv[k] & 0xFFFFu, (((dmask >> k) & 1u) & (cv[k] - fhs <= lim3 ? 1u : 0u)) != 0u);
-    }
-    if (longm) best = 0;  // a long candidate always wins
-    while (longm && best < limit) {
-        const uint32_t k = (uint32_t)__builtin_ctz(longm);
-        longm &= longm - 1u;
-        const uint32_t q = cand(k) & 0xFFFFu;
-        uint32_t m = 7;
-        for (;;) {
-            const uint32_t x = ld32u(s_in, q + m) ^ ld32u(s_in, p + m);
-            if (x) {
-                m += (uint32_t)__builtin_ctz(x) >> 3;
-                break;
-            }
-            m += 4;
-            if (m >= limit) break;
-        }
-        if (m > limit) m = limit;
-        if (m > best) {
-            best = m;
-            bpos = q;
-        }
-    }
-    best_out = best;
-    bpos_out = bpos;
-}
-
 // One pass of a stable LSD radix partition of the searched positions by
 // NB_LOG2 bits of their hash (starting at bit `shift`): out[] lists the
 // positions of in[] (or 0..P-1) grouped by key, each group in input order.
@@ -440,180 +357,6 @@ __device__ void bucket_sort(const uint8_t *s_in, uint32_t P, uint16_t *tmp, uint
     stable_partition<W, 8>(s_in, P, tmp, gl, 4, cntB, wsum, subB, nullptr, nullptr, true);
 }
 
-
-// ---- Ring tiles (the 64 KiB kernel): sort + best match without global scratch ----
-// The searched positions are taken in kRtPasses passes over bucket ranges (bucket >> 8 = the pass,
-// bucket & 255 = the key).  A pass keeps per key the 16 latest entries (`ring`, slot = rank & 15)
-// and the count so far mod 256 (`rcnt`), exactly the reference's hash_table / hash_counter rows
-// (quicklz.c:316-331, 366-372) for 256 of its 4096 buckets.  It reads the pass's positions in
-// position order in tiles of at most kRtCap (a 4-bit pass id per position, built once, finds them),
-// sorts a tile by key, stable in position, entirely in LDS, and matches every entry of the tile at
-// once: candidate k (rank r - 1 - k) is the tile entry k + 1 places before it while that has the
-// same key, else the ring slot of that rank.  Then the tile's last 16 entries per key go into the
-// ring.  Best lengths go to global memory (u8 per position, the workgroup's slot) and come back
-// into LDS once the block's passes are done: the 128 KB of s_in + s_l8 leave 98 KB for all this.
-#ifndef QLZX_RING_TILES
-#define QLZX_RING_TILES 1
-#endif
-constexpr bool kRingTiles = QLZX_RING_TILES;
-constexpr uint32_t kRtPasses = 16, kRtKeys = QLZX_BUCKETS / kRtPasses;
-template <uint32_t W>
-struct RtL {  // byte offsets in the region after s_in (where s_l8 and s_scr live afterwards)
-    static constexpr uint32_t NIB = 0;                                    // u32[8192]: pass id per position
-    static constexpr uint32_t RING = NIB + 65536 / 2;                     // u32[256][16]
-    static constexpr uint32_t CNT = RING + kRtKeys * 16 * 4;              // u32 [key][wave] counters
-    static constexpr uint32_t TST = CNT + cslots(kRtKeys, W) * 4;         // u32[257]: tile start per key
-    static constexpr uint32_t RCNT = (TST + (kRtKeys + 1) * 4 + 15) & ~15u;  // u32[256]: count mod 256
-    static constexpr uint32_t ES = RCNT + kRtKeys * 4;                    // u32[CAPE]: sorted tile
-    static constexpr uint32_t CAPE = 4800;
-    static constexpr uint32_t EU = ES + CAPE * 4;                         // u16[CAPE]: tile in position order
-    static constexpr uint32_t BYTES = EU + CAPE * 2;
-};
-
-// Bit 4j+3 set iff nibble j of x is zero (exact: no carry crosses a nibble).
-__device__ __forceinline__ uint32_t zero_nibbles(uint32_t x) {
-    return ~(((x & 0x77777777u) + 0x77777777u) | x | 0x77777777u);
-}
-
-template <uint32_t W, bool COMPACT>
-__device__ void ring_tile_matches(const uint8_t *s_in, uint32_t n, uint32_t P, uint8_t *rg, uint64_t *wsum,
-                                  uint32_t *s_end, uint8_t *l8g, uint16_t *goff, unsigned long long *sub) {
-    using L = RtL<W>;
-    constexpr uint32_t T = 64 * W, CAPE = L::CAPE;
-    uint32_t *const nib = (uint32_t *)(rg + L::NIB);
-    uint32_t *const ring = (uint32_t *)(rg + L::RING);
-    uint32_t *const cnt = (uint32_t *)(rg + L::CNT);
-    uint32_t *const tst = (uint32_t *)(rg + L::TST);
-    uint32_t *const rcnt = (uint32_t *)(rg + L::RCNT);
-    uint32_t *const es = (uint32_t *)(rg + L::ES);
-    uint16_t *const eu = (uint16_t *)(rg + L::EU);
-    uint32_t tid = tid_here();
-#ifdef QLZX_PROFILE
-    if (sub) sub[7] = __builtin_amdgcn_s_memtime();
-#endif
-    // pass id of every searched position, 8 per word (s_in is zero padded past n + 10)
-    for (uint32_t k = tid; k < (P + 7) / 8; k += T) {
-        const uint32_t *w = (const uint32_t *)(s_in + 8 * k);
-        const uint32_t a = w[0], b = w[1], c = w[2];
-        uint32_t v = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++) {
-            const uint32_t f = (j < 4 ? __builtin_amdgcn_alignbyte(b, a, j) : __builtin_amdgcn_alignbyte(c, b, j - 4)) &
-                               0xFFFFFFu;
-            v |= (hash12(f) >> 8) << (4 * j);
-        }
-        nib[k] = v;
-    }
-    __syncthreads();
-    SUB_MARK(0);
-    for (uint32_t g = 0; g < kRtPasses; g++) {
-        tid = tid_here();
-        const uint32_t lane = tid & 63, wave = tid >> 6;
-        const uint64_t ltm = (1ull << lane) - 1ull;
-        if (tid < kRtKeys) rcnt[tid] = 0;
-        const uint32_t gm = g * 0x11111111u;
-        for (uint32_t pc = 0; pc < P;) {  // workgroup-uniform
-            // 1. the pass's positions in [pc, P), in position order, up to CAPE of them
-            const uint32_t wa = pc >> 3, wb = (P + 7) >> 3;
-            const uint32_t per = (wb - wa + T - 1) / T;
-            const uint32_t t0 = min(wb, wa + tid * per), t1 = min(wb, t0 + per);
-            auto hits = [&](uint32_t k) {
-                uint32_t z = zero_nibbles(nib[k] ^ gm);
-                const uint32_t lo = 8 * k;
-                if (lo < pc) z &= ~0u << (4 * (pc - lo));
-                if (lo + 8 > P) z &= (1u << (4 * (P - lo))) - 1u;  // P - lo in 1..7
-                return z;
-            };
-            uint32_t c = 0;
-            for (uint32_t k = t0; k < t1; k++) c += (uint32_t)__popc(hits(k));
-            uint64_t tot;
-            uint32_t idx = (uint32_t)block_scan_excl<W>(c, wsum, tot);
-            const uint32_t m = (uint32_t)tot, mt = m < CAPE ? m : CAPE;
-            for (uint32_t k = t0; k < t1 && idx <= CAPE; k++) {
-                for (uint32_t z = hits(k); z && idx <= CAPE; z &= z - 1u, idx++) {
-                    const uint32_t q = 8 * k + ((uint32_t)__builtin_ctz(z) >> 2);
-                    if (idx < CAPE) eu[idx] = (uint16_t)q;
-                    else *s_end = q;  // the first position of the next tile
-                }
-            }
-            for (uint32_t k = tid; k < cslots(kRtKeys, W); k += T) cnt[k] = 0;
-            __syncthreads();
-            const uint32_t pe = m > CAPE ? *s_end : P;
-            SUB_MARK(1);
-            // 2. stable counting sort of the tile by key: wave w owns entries [r0, r1)
-            const uint32_t per2 = (mt + T - 1) / T * 64;
-            const uint32_t r0 = min(mt, wave * per2), r1 = min(mt, r0 + per2);
-            for (uint32_t j = r0 + lane; j < r1; j += 64)
-                atomicAdd(&cnt[cslot<W>((hash12(fetch24(s_in, eu[j])) & (kRtKeys - 1)) * W + wave)], 1u);
-            __syncthreads();
-            {
-                constexpr uint32_t CPT = kRtKeys * W / T;
-                static_assert(CPT >= 1 && W % CPT == 0 && CPT * T == kRtKeys * W, "counter layout");
-                uint32_t v[CPT], sum = 0;
-#pragma unroll
-                for (uint32_t j = 0; j < CPT; j++) sum += (v[j] = cnt[cslot<W>(CPT * tid + j)]);
-                uint64_t tot2;
-                uint32_t ex = (uint32_t)block_scan_excl<W>(sum, wsum, tot2);
-                if ((CPT * tid) % W == 0) tst[CPT * tid / W] = ex;
-#pragma unroll
-                for (uint32_t j = 0; j < CPT; j++) {
-                    cnt[cslot<W>(CPT * tid + j)] = ex;
-                    ex += v[j];
-                }
-                if (tid == 0) tst[kRtKeys] = mt;
-            }
-            __syncthreads();
-            SUB_MARK(2);
-            for (uint32_t base = r0; base < r1; base += 64) {  // wave-uniform
-                const uint32_t j = base + lane;
-                const bool valid = j < r1;
-                const uint32_t q = valid ? (uint32_t)eu[j] : 0u;
-                const uint32_t f = fetch24(s_in, q);
-                const uint32_t key = valid ? hash12(f) & (kRtKeys - 1) : 0u;
-                const uint64_t peers = match_peers<8>(key, __ballot(valid));
-                const uint32_t intra = (uint32_t)__popcll(peers & ltm);
-                uint32_t cur = 0;
-                if (valid) cur = cnt[cslot<W>(key * W + wave)];
-                // every lane's read is issued before the leader's write (in-order LDS per wave)
-                if (valid && intra == 0) cnt[cslot<W>(key * W + wave)] = cur + (uint32_t)__popcll(peers);
-                if (valid) es[cur + intra] = q | ((f >> 12) << 16);
-            }
-            __syncthreads();
-            SUB_MARK(3);
-            // 3. best match of every tile entry
-            for (uint32_t eb = tid - lane; eb < mt; eb += T) {  // wave-uniform
-                const uint32_t e = eb + lane;
-                if (e >= mt) continue;
-                const uint32_t self = es[e], p = self & 0xFFFFu;
-                const uint32_t key = hash12(fetch24(s_in, p)) & (kRtKeys - 1);
-                const uint32_t j = e - tst[key], base = rcnt[key] + j;
-                const uint32_t rm = base & 255u, d = rm < 16u ? rm : 16u;
-                const uint32_t *const rk = ring + 16 * key;
-                uint32_t best, bpos;
-                best_of<COMPACT>(s_in, n, p, self, d,
-                                 [&](uint32_t k) { return k < j ? es[e - 1u - k] : rk[(base - 1u - k) & 15u]; }, best,
-                                 bpos);
-                l8g[p] = (uint8_t)best;  // 0 = literal, else 3..255
-                if (best) goff[p] = (uint16_t)(p - bpos);
-            }
-            __syncthreads();
-            SUB_MARK(4);
-            // 4. each key's last 16 tile entries into its ring, then the counts
-            for (uint32_t e = tid; e < mt; e += T) {
-                const uint32_t self = es[e];
-                const uint32_t key = hash12(fetch24(s_in, self & 0xFFFFu)) & (kRtKeys - 1);
-                const uint32_t j = e - tst[key];
-                if (j + 16u >= tst[key + 1] - tst[key]) ring[16 * key + ((rcnt[key] + j) & 15u)] = self;
-            }
-            __syncthreads();
-            if (tid < kRtKeys) rcnt[tid] += tst[tid + 1] - tst[tid];
-            SUB_MARK(5);
-            pc = pe;  // (the next tile's scans sync before rcnt is read again)
-        }
-        __syncthreads();
-    }
-}
-
 template <uint32_t CAP>
 struct WgCfg {
     static constexpr uint32_t T = CAP / 64;  // threads = walkers (one 64-position segment each)
@@ -627,7 +370,6 @@ struct WgCfg {
     static constexpr uint32_t SC4 = 2 * NCW;         // phase 4 control words + positions
     static constexpr uint32_t SC3 = (T + 2) + 2 * T;  // phase 3 exits + serial-walk segment bits
     static constexpr uint32_t SCR = SC1 > SC4 ? (SC1 > SC3 ? SC1 : SC3) : (SC4 > SC3 ? SC4 : SC3);
-    static constexpr uint32_t SCR_RT = SC4 > SC3 ? SC4 : SC3;  // ring tiles: no phase-1 counters here
     // gl u32[CAP] (sorted positions | fetch[23:12] << 16) | goff u16[CAP] | bst u16[4096]
     static constexpr size_t SLOT_BYTES = (size_t)CAP * 6 + QLZX_BUCKETS * 2;
     static_assert((1u << BM_LOG2) / 8 <= U_B, "proof bitmap overlays s_in|s_l8");
@@ -649,18 +391,13 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                                                          uint8_t *ws, uint32_t *ticket) {
     using C = WgCfg<CAP>;
     constexpr uint32_t T = C::T, W = C::W;
-    // RT (ring tiles, the 64 KiB kernel): s_in | one region that holds the ring-tile state during
-    // phases 1-2 and s_l8 | s_scr afterwards
-    constexpr bool RT = kRingTiles && CAP == 65536;
-    constexpr uint32_t RT_B = RtL<W>::BYTES > C::L8_B + 4 * C::SCR_RT ? RtL<W>::BYTES : C::L8_B + 4 * C::SCR_RT;
-    __shared__ __attribute__((aligned(16))) uint8_t s_u[RT ? C::IN_B + RT_B : C::U_B];
-    __shared__ __attribute__((aligned(16))) uint32_t s_scr_a[RT ? 1 : C::SCR];
+    __shared__ __attribute__((aligned(16))) uint8_t s_u[C::U_B];
+    __shared__ __attribute__((aligned(16))) uint32_t s_scr[C::SCR];
     __shared__ uint64_t s_wsum[W];
-    __shared__ uint32_t s_misc[24];  // [0] next group, [1] proof count, [4..] CRC stripes, [23] tile end
-    constexpr bool BL = kBstLds && CAP == 65536 && !RT;  // (the smaller kernels' occupancy is LDS-bound)
+    __shared__ uint32_t s_misc[24];  // [0] next group, [1] proof count, [4..] CRC stripes
+    constexpr bool BL = kBstLds && CAP == 65536;  // (the smaller kernels' occupancy is LDS-bound)
     __shared__ uint16_t s_bst[BL ? QLZX_BUCKETS : 1];
     uint8_t *const s_in = s_u, *const s_l8 = s_u + C::IN_B;
-    uint32_t *const s_scr = RT ? (uint32_t *)(s_u + C::IN_B + C::L8_B) : s_scr_a;
 
     uint32_t *gl = (uint32_t *)(ws + (size_t)blockIdx.x * C::SLOT_BYTES);
     uint16_t *goff = (uint16_t *)(gl + CAP);
@@ -859,16 +596,6 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
 #else
                 unsigned long long *subA = nullptr, *subB = nullptr;
 #endif
-                if constexpr (RT) {
-                    // ---- 1 + 2. ring tiles (above): sort and best match in LDS, lengths via the slot ----
-                    (void)subB;
-                    uint8_t *const l8g = (uint8_t *)gl;
-                    PROF_MARK(2);
-                    if (cmode) ring_tile_matches<W, true>(s_in, n, P, s_l8, s_wsum, &s_misc[23], l8g, goff, subA);
-                    else ring_tile_matches<W, false>(s_in, n, P, s_l8, s_wsum, &s_misc[23], l8g, goff, subA);
-                    QLZX_TID_REFRESH();
-                    for (uint32_t o = tid * 16; o < P; o += T * 16) *(uint4 *)(s_l8 + o) = *(const uint4 *)(l8g + o);
-                } else {
                 bucket_sort<W, C::L8_B>(s_in, P, goff, gl, bst, s_scr, (uint32_t *)s_l8, s_wsum, subA, subB);
 
                 PROF_MARK(2);  // 2: sort by bucket
@@ -918,9 +645,76 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                     const uint32_t p = self & 0xFFFFu;
                     const uint32_t rm = (t - (uint32_t)bst[hash12(fetch24(s_in, p))]) & 255u;
                     const uint32_t d = rm < 16u ? rm : 16u;
-                    uint32_t best, bpos;
-                    best_of<decltype(compact)::value>(s_in, n, p, self, d, [&](uint32_t k) { return stg[15u + lane - k]; },
-                                                      best, bpos);
+                    const uint32_t limit = min(255u, n - 4u - p);  // quicklz.c:310
+                    // First pass: bytes 3..6 of every candidate against this position's, all
+                    // LDS reads independent.  A mismatch there gives the exact length; the
+                    // candidates equal through byte 6 ("long") are extended afterwards, most
+                    // recent first -- they beat every short one, and ties stay with the more
+                    // recent (larger) position.
+                    const uint32_t P3 = ld32u(s_in, p + 3);
+                    uint32_t best = 0, bpos = 0, longm = 0;
+                    auto first = [&](uint32_t k, uint32_t q, bool ok) {
+                        const uint32_t x = ld32u(s_in, q + 3) ^ P3;
+                        const uint32_t m = min(x ? 3u + ((uint32_t)__builtin_ctz(x) >> 3) : 7u, limit);
+                        if (ok && !x && limit > 7u) longm |= 1u << k;
+                        else if (ok && m > best) {
+                            best = m;
+                            bpos = q;
+                        }
+                    };
+                    // A candidate can match when it is in the bucket (k < d) with the same
+                    // fetch[23:12] (same bucket + same fetch[23:12] = same 3 bytes) and
+                    // o < src - MINOFFSET (q + 3 <= p): with fhs = fetch[23:12] << 16, the word
+                    // c - fhs is q when the fetch bits agree and >= 2^16 otherwise, so one
+                    // subtraction and one compare against p - 3 test both (no candidate at p < 3).
+                    const uint32_t fhs = self & 0xFFFF0000u, lim3 = p - 3u;
+                    const uint32_t dmask = p >= 3u ? (1u << d) - 1u : 0u;
+                    if constexpr (decltype(compact)::value) {
+                        uint32_t okm = 0;
+#pragma unroll
+                        for (uint32_t k = 0; k < 16; k++) {
+                            const uint32_t c = stg[15u + lane - k];
+                            okm |= (c - fhs <= lim3) ? 1u << k : 0u;
+                        }
+                        okm &= dmask;
+                        if (__ballot((uint32_t)__popc(okm) > kMatchCompactMax) == 0ull) {  // wave-uniform
+                            for (uint32_t t2 = okm; t2; t2 &= t2 - 1u) {  // set bits, most recent first
+                                const uint32_t k = (uint32_t)__builtin_ctz(t2);
+                                first(k, stg[15u + lane - k] & 0xFFFFu, true);
+                            }
+                        } else {
+#pragma unroll
+                            for (uint32_t k = 0; k < 16; k++) first(k, stg[15u + lane - k] & 0xFFFFu, (okm >> k) & 1u);
+                        }
+                    } else {
+                        uint32_t cand[16];  // most recent first
+#pragma unroll
+                        for (uint32_t k = 0; k < 16; k++) cand[k] = stg[k < d ? 15u + lane - k : 16u + lane];
+#pragma unroll
+                        for (uint32_t k = 0; k < 16; k++)
+                            first(k, cand[k] & 0xFFFFu, (((dmask >> k) & 1u) & (cand[k] - fhs <= lim3 ? 1u : 0u)) != 0u);
+                    }
+                    if (longm) best = 0;  // a long candidate always wins
+                    while (longm && best < limit) {
+                        const uint32_t k = (uint32_t)__builtin_ctz(longm);
+                        longm &= longm - 1u;
+                        const uint32_t q = stg[15u + lane - k] & 0xFFFFu;
+                        uint32_t m = 7;
+                        for (;;) {
+                            const uint32_t x = ld32u(s_in, q + m) ^ ld32u(s_in, p + m);
+                            if (x) {
+                                m += (uint32_t)__builtin_ctz(x) >> 3;
+                                break;
+                            }
+                            m += 4;
+                            if (m >= limit) break;
+                        }
+                        if (m > limit) m = limit;
+                        if (m > best) {
+                            best = m;
+                            bpos = q;
+                        }
+                    }
                     s_l8[p] = (uint8_t)best;  // 0 = literal, else 3..255
                     if (best) goff[p] = (uint16_t)(p - bpos);
                   }
@@ -928,7 +722,6 @@ __global__ void __launch_bounds__(CAP / 64) k_encode_wg(qlzx_blocks b, uint32_t 
                 };
                 if (cmode) best_matches(std::true_type{});
                 else best_matches(std::false_type{});
-                }
             }
             __syncthreads();
 

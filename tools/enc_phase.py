@@ -56,4 +56,3 @@ for kind in os.environ.get("KINDS", "random,noisy,text,zeros").split(","):
           flush=True)
     q = prof.cpu().numpy()[24:40] / (n * max(waves, 1))
     print("   sort passes (zero, count, scan, scatter):", [int(x) for x in q[0:4]], [int(x) for x in q[8:12]], flush=True)
-    print("   ring tiles (pass ids, select, count+scan, scatter, match, ring):", [int(x) for x in q[0:6]], flush=True)
