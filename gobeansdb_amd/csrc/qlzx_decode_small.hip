@@ -158,6 +158,7 @@ __device__ __forceinline__ bool small_decode(SmallLds &L, const uint8_t *src, ui
     for (uint32_t x = hdr + tid; x + 4 <= csize; x += kSoloWG)
         if (sb[x + 3] >> 7) L.p.ja[w++] = (uint16_t)x;
     __syncthreads();
+    SM_SUB(2);
     // 1b. parse the group at every candidate (one dependent LDS read per match token).  All
     //     lanes stay busy: a lane whose chain ends takes the next unparsed candidate from a
     //     shared cursor, and a step is a handful of VALU ops (codes from cb, C2 folded in).

@@ -41,6 +41,8 @@ for n in (4096, 16384, 32768, 65536):
         ph = {nm: round(p[24 + j] / k) for j, nm in enumerate(names_small)}
         ph["(stage)"] = round(p[16] / k)
         ph["(stage+classify)"] = round(p[17] / k)
+        if p[18]:
+            ph["(.. +candidates)"] = round(p[18] / k)
     else:
         k = max(p[23], 1)
         ph = {nm: round(p[16 + j] / k) for j, nm in enumerate(names[:7])}
