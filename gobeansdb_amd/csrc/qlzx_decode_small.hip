@@ -28,6 +28,9 @@ constexpr uint32_t kSmOwn = 16;                  // output bytes per thread per 
 constexpr uint32_t kSmSeg = kSmD / (kSoloWG * kSmOwn);  // 2 segments of 16 KiB
 constexpr uint32_t kSmIT = 8;                    // items per thread per decode round
 constexpr uint32_t kSmEnd = 0xA0, kSmBad = 0xFF;  // info codes besides FULL (35..128)
+#ifndef QLZX_SM_PAIR  // step 1b takes a second match token per step when its code is in the same dword
+#define QLZX_SM_PAIR 1
+#endif
 static_assert(kSmC % 16 == 0 && kSmC + 64 < 65536, "u16 positions");
 
 struct SmallLds {
@@ -178,10 +181,32 @@ __device__ __forceinline__ bool small_decode(SmallLds &L, const uint8_t *src, ui
             const uint32_t k = min((uint32_t)__builtin_ctz(mrem | 0x80000000u), 30u);  // no match left: 30
             bool fin = kend <= k || !mrem;   // ends before the next match / item 31, or FULL
             if (!fin) {
+#if QLZX_SM_PAIR
+                // the codes of 4 bytes from this token's: a next match whose first byte is among
+                // them (its code sits k2 - k + c bytes on) is taken in the same step
+                const uint32_t a = x4 + k + ex;
+                const uint32_t *cbw = (const uint32_t *)L.cb;
+                const uint32_t w = __builtin_amdgcn_alignbyte(cbw[(a >> 2) + 1], cbw[a >> 2], a & 3u);
+                c = w & 0xffu;
+                fin = c > 3;  // C2
+                if (!fin) {
+                    ex += c;
+                    mrem &= mrem - 1;
+                    const uint32_t k2 = min((uint32_t)__builtin_ctz(mrem | 0x80000000u), 30u);
+                    const uint32_t d = k2 - k + c;
+                    if (lim - ex > k2 && mrem != 0 && d <= 3) {
+                        c = (w >> (8 * d)) & 0xffu;
+                        fin = c > 3;  // C2
+                        ex += fin ? 0u : c;
+                        mrem &= fin ? mrem : mrem - 1;
+                    }
+                }
+#else
                 c = L.cb[x4 + k + ex];
                 fin = c > 3;  // C2
                 ex += fin ? 0u : c;
                 mrem &= fin ? mrem : mrem - 1;
+#endif
             }
             if (fin) {
                 const uint32_t ke = lim - ex;

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Small-block decoder, step 1b with interleaved candidate chains: parity tests, phase stamps
-# (libqlzx_prof.so vs libqlzx_pc0.so = one chain with a cursor), then single-call latency and the
-# 16-pthread aggregate for one chain (libqlzx_c0.so), 3 (libqlzx.so) and 4 (libqlzx_c4.so).
+# Small-block decoder step 1b A/B: parity tests, phase stamps (libqlzx_prof.so vs libqlzx_pc0.so),
+# then single-call latency and the 16-pthread aggregate, variant (libqlzx.so) against HEAD
+# (libqlzx_c0.so).  Round 5: interleaved chains, static candidates, then token pairs.
 set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp
 O=gpurun_out/r05sc; mkdir -p $O
@@ -13,7 +13,7 @@ for l in libqlzx_pc0.so libqlzx_prof.so; do
 done
 timeout -k 10 200 python -u tools/bench_single.py --calls 1000 --values 1024 --threads 0 --dump $O --out $O/single_dump.json > /dev/null 2>&1 || exit 1
 gcc -O2 -pthread -o $O/mt_single tools/mt_single.c -ldl || exit 1
-for l in libqlzx_c0.so libqlzx.so libqlzx_c4.so libqlzx_c0.so libqlzx.so; do
+for l in libqlzx_c0.so libqlzx.so libqlzx_c0.so libqlzx.so; do
   QLZX_LIB=$PWD/gobeansdb_amd/$l timeout -k 10 300 python -u tools/bench_single.py --calls 1000 --values 1024 --threads 0 --out $O/single_$l.json 2>&1 | grep -v amdgpu.ids > $O/single_$l.txt || exit 1
   python3 -c "
 import json; d=json.load(open('$O/single_$l.json'))
