@@ -158,6 +158,11 @@ def main():
     p.add_argument("--seed", type=int, default=2026)
     p.add_argument("--cpu-seconds", type=float, default=8.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--pipe-mib", type=int, default=4096,
+                   help="end-to-end legs: pieces cut at record starts into parts of about this size (smaller "
+                        "parts shorten the exposed first H2D, but each replay call reads its record counts "
+                        "back to size its outputs: 512 MiB parts gave 36 GiB/s for the hints leg, 128 MiB 21, "
+                        "whole 4000 MiB pieces 46)")
     p.add_argument("--pin-records", type=int, default=1024,
                    help="records per chunk compared with the oracle inside the correctness gate")
     a = p.parse_args()
@@ -192,7 +197,8 @@ def run(a, rank: int, world: int, dev):
       corpus digest, the same at every N);
     * device-only: the rank's pieces from the resident chunks, a.steps passes;
     * end to end: the same pieces pipelined from pinned host memory (H2D of piece i+1, replay of
-      piece i, D2H of piece i-1's decompressed values on three streams).
+      piece i, D2H of piece i-1's decompressed values on three streams), and again with only the
+      hint fields going back (buildHintFromData frees each body after Getvhash).
     Returns the record on rank 0 (max-over-ranks times, summed bytes; CPU leg at N = 1 only)."""
     from gobeansdb_amd import replay, batch, shard
     t0 = time.time()
@@ -269,7 +275,21 @@ def run(a, rank: int, world: int, dev):
     # ---- end to end, pipelined: H2D of piece i+1 || replay of piece i || D2H of piece i-1 ----
     # three streams, two device slots and two pinned output slots (PCIe is full duplex); only
     # decompressed values travel back (raw values are bytes the host already holds)
-    slot_b = max([hi - lo for _, lo, hi in pieces], default=1)
+    # the end-to-end legs move each piece in parts of about --pipe-mib, cut at record starts
+    # (every record start of the generated chunks is a cut point; a part is a .data stream of its own)
+    parts = []
+    step_b = max(getattr(a, "pipe_mib", 4096), 1) << 20
+    for k, lo, hi in pieces:
+        ro = chunks[k]["rec_off"].astype(np.int64)
+        x = lo
+        while x < hi:
+            want = x + step_b
+            idx = int(np.searchsorted(ro, want, side="left"))  # first record start at or past want
+            y = int(ro[idx]) if want < hi and idx < len(ro) else hi
+            y = min(y, hi)
+            parts.append((k, x, y))
+            x = y
+    slot_b = max([hi - lo for _, lo, hi in parts], default=1)
     s_h2d, s_cmp, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     dslot = [torch.empty(slot_b, dtype=torch.uint8, device=dev) for _ in range(2)]
     hslot = [torch.empty(max(out_cap, 1), dtype=torch.uint8).pin_memory() for _ in range(2)]
@@ -278,18 +298,18 @@ def run(a, rank: int, world: int, dev):
     ev_out = [torch.cuda.Event(), torch.cuda.Event()]     # D2H done with host slot
 
     def h2d(i):
-        k, lo, hi = pieces[i]
+        k, lo, hi = parts[i]
         dslot[i & 1][: hi - lo].copy_(chunks[k]["pinned"][lo:hi], non_blocking=True)
         ev_in[i & 1].record(s_h2d)
 
     sync_all()
     t = time.perf_counter()
-    if pieces:
+    if parts:
         with torch.cuda.stream(s_h2d):
             h2d(0)
-    for i, (k, lo, hi) in enumerate(pieces):
+    for i, (k, lo, hi) in enumerate(parts):
         j = i & 1
-        if i + 1 < len(pieces):   # prefetch the next piece while this one replays
+        if i + 1 < len(parts):   # prefetch the next piece while this one replays
             with torch.cuda.stream(s_h2d):
                 if i >= 1:
                     s_h2d.wait_event(ev_used[j ^ 1])
@@ -308,7 +328,45 @@ def run(a, rank: int, world: int, dev):
             ev_out[j].record(s_d2h)
     sync_all()
     pipe_s = time.perf_counter() - t
-    dev_wall, dev_ev, pipe_s = shard.max_over_ranks([dev_wall, dev_ev, pipe_s], device=dev)
+
+    # ---- end to end as buildHintFromData needs it (store/bucket.go:89-117): the decompressed
+    # body only feeds Getvhash and is freed (p.Free()), so per record only the hint fields travel
+    # back -- offset, the stored header (ver, ksz, vsz: the record size) and vhash ----
+    hmax = max([int(np.searchsorted(chunks[k]["rec_off"].astype(np.int64), hi)
+                    - np.searchsorted(chunks[k]["rec_off"].astype(np.int64), lo)) for k, lo, hi in parts], default=1)
+    hint_host = [dict(off=torch.empty(max(hmax, 1), dtype=torch.int64).pin_memory(),
+                      hdr=torch.empty((max(hmax, 1), 6), dtype=torch.int32).pin_memory(),
+                      vh=torch.empty(max(hmax, 1), dtype=torch.int32).pin_memory()) for _ in range(2)]
+    sync_all()
+    t = time.perf_counter()
+    if parts:
+        with torch.cuda.stream(s_h2d):
+            h2d(0)
+    for i, (k, lo, hi) in enumerate(parts):
+        j = i & 1
+        if i + 1 < len(parts):
+            with torch.cuda.stream(s_h2d):
+                if i >= 1:
+                    s_h2d.wait_event(ev_used[j ^ 1])
+                h2d(i + 1)
+        with torch.cuda.stream(s_cmp):
+            s_cmp.wait_event(ev_in[j])
+            r = replay.replay(dslot[j][: hi - lo], workspace=ws, stream=s_cmp)
+            ev_used[j].record(s_cmp)
+        with torch.cuda.stream(s_d2h):
+            s_d2h.wait_event(ev_used[j])
+            if i >= 2:
+                s_d2h.wait_event(ev_out[j])
+            hh, n = hint_host[j], r.n
+            hh["off"][:n].copy_(r.offset, non_blocking=True)
+            hh["hdr"][:n].copy_(r.header, non_blocking=True)
+            hh["vh"][:n].copy_(r.vhash, non_blocking=True)
+            for tsr in (r.offset, r.header, r.vhash):
+                tsr.record_stream(s_d2h)
+            ev_out[j].record(s_d2h)
+    sync_all()
+    hint_s = time.perf_counter() - t
+    dev_wall, dev_ev, pipe_s, hint_s = shard.max_over_ranks([dev_wall, dev_ev, pipe_s, hint_s], device=dev)
     tot = shard.sum_over_ranks({"chunk": share, "out": out_mine, "records": nrec_mine, "pieces": len(pieces)},
                                device=dev)
     cpu = None
@@ -348,8 +406,15 @@ def run(a, rank: int, world: int, dev):
         "end_to_end_pipelined": {"total_gib": round(tot["chunk"] / 2**30, 2),
                                  "gib_per_s_chunk": round(tot["chunk"] / pipe_s / 2**30, 2),
                                  "seconds": round(pipe_s, 2),
-                                 "note": "each rank's pieces: pinned H2D of piece i+1, replay of piece i and pinned "
-                                         "D2H of piece i-1's decompressed values on three streams"},
+                                 "parts": len(parts), "part_mib": getattr(a, "pipe_mib", 4096),
+                                 "note": "each rank's pieces in parts cut at record starts: pinned H2D of part i+1, "
+                                         "replay of part i and pinned D2H of part i-1's decompressed values on three "
+                                         "streams"},
+        "end_to_end_hints": {"gib_per_s_chunk": round(tot["chunk"] / hint_s / 2**30, 2),
+                             "seconds": round(hint_s, 2),
+                             "note": "as buildHintFromData (store/bucket.go:89-117): the same pipeline, but the "
+                                     "decompressed bodies stay on the device (they only feed Getvhash, p.Free()); "
+                                     "per record offset, stored header and vhash go back (pinned D2H)"},
         "data": "synthetic",
         "cpu_baseline": cpu,
     }
