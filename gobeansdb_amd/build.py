@@ -44,16 +44,32 @@ def _stale() -> bool:
 PROF_OUT = os.path.join(HERE, "libqlzx_prof.so")
 
 
-def _compile(out: str, extra: list[str], verbose: bool) -> None:
-    # --offload-compress: the gfx950 code object is stored zstd-compressed (1.1 MB instead of
-    # 3.8 MB; the HIP runtime inflates it at load)
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "--offload-compress",
-           "-Wall", "-Wno-unused-function", "-Wno-unused-parameter", f"-DQLZX_SRC_HASH=\"{source_hash()}\"", *extra,
-           "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp",
-           os.path.join(CSRC, "qlzx_api.hip")]
+# K2 without its CRC prologue (k_dec_chunk4<false>) is compiled in a translation unit of its own
+# with this machine-scheduler strategy (csrc/qlzx_k2.hip; profiles/r05_sched_strategy_ab.txt)
+K2_SCHED = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
+
+
+def _compile(out: str, extra: list[str], verbose: bool, split: bool = True) -> None:
+    # --offload-compress: the gfx950 code object is stored zstd-compressed (1.1 MB instead of
+    # 3.8 MB; the HIP runtime inflates it at load)
+    base = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "--offload-compress", "-Wall",
+            "-Wno-unused-function", "-Wno-unused-parameter", "-I", os.path.join(ROOT, "include")]
+    api = [f"-DQLZX_SRC_HASH=\"{source_hash()}\"", *extra]
+    if not split:  # one translation unit (the profile build: its stamps need qlzx_api.hip's g_prof)
+        _run([*base, "-shared", *api, "-o", out + ".tmp", os.path.join(CSRC, "qlzx_api.hip")], verbose)
+    else:
+        oa, ok2 = out + ".api.o", out + ".k2.o"
+        _run([*base, "-c", *api, "-DQLZX_SPLIT_K2=1", "-o", oa, os.path.join(CSRC, "qlzx_api.hip")], verbose)
+        _run([*base, "-c", *extra, *K2_SCHED, "-o", ok2, os.path.join(CSRC, "qlzx_k2.hip")], verbose)
+        _run(["hipcc", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", out + ".tmp", oa, ok2], verbose)
+        for f in (oa, ok2):
+            os.remove(f)
     os.replace(out + ".tmp", out)
 
 
@@ -62,7 +78,7 @@ def build(force: bool = False, verbose: bool = False, profile: bool = False) -> 
     if force or _stale():
         _compile(OUT, [], verbose)
     if profile:
-        _compile(PROF_OUT, ["-DQLZX_PROFILE", "-DQLZX_SP_WAVES_PER_EU=1"], verbose)
+        _compile(PROF_OUT, ["-DQLZX_PROFILE", "-DQLZX_SP_WAVES_PER_EU=1"], verbose, split=False)
     return OUT
 
 

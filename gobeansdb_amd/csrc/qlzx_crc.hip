@@ -226,6 +226,7 @@ __device__ __forceinline__ uint32_t wave_crc_rep(const uint32_t *tab, const uint
     return __shfl(c, 0, 64);
 }
 
+#ifndef QLZX_K2_ONLY
 __global__ void __launch_bounds__(256) k_crc32(const uint8_t *src, const uint64_t *off,
                                                const uint32_t *len, uint32_t n,
                                                const uint32_t *init, uint32_t final_xor,
@@ -239,6 +240,7 @@ __global__ void __launch_bounds__(256) k_crc32(const uint8_t *src, const uint64_
     const uint32_t reg = wave_crc(tab, src + off[i], len[i], init ? init[i] : 0xffffffffu, lane);
     if (lane == 0) out[i] = reg ^ final_xor;
 }
+#endif  // QLZX_K2_ONLY
 
 // ---------------- synthetic workloads ----------------
 __device__ __forceinline__ uint64_t sm64(uint64_t &s) {
@@ -288,6 +290,7 @@ __device__ void gen_image(uint64_t s, const uint8_t *vocab, const uint32_t *voff
     }
 }
 
+#ifndef QLZX_K2_ONLY
 __global__ void __launch_bounds__(64) k_synth(int kind, uint64_t seed, uint64_t first, uint8_t *dst,
                                               const uint64_t *off, const uint32_t *len, uint32_t n,
                                               const uint8_t *vocab, const uint32_t *voff,
@@ -298,5 +301,6 @@ __global__ void __launch_bounds__(64) k_synth(int kind, uint64_t seed, uint64_t 
     if (kind == 0) gen_text(s, vocab, voff, cdf, nw, dst + off[i], len[i]);
     else gen_image(s, vocab, voff, cdf, nw, dst + off[i], len[i]);
 }
+#endif  // QLZX_K2_ONLY
 
 }  // namespace qlzx

@@ -34,6 +34,7 @@ namespace qlzx {
 // round.  Here lanes drift apart in stream position and the wave pays kmax steps per iteration.
 // c2 25.1-25.3 -> 24.7-24.9 ms at kmax 16; c4 346 -> 377 GiB/s at kmax 10
 // (tools/gpu_r5lr3.sh, profiles/r05_k1_lane_ring_ab.txt).
+#ifndef QLZX_K2_ONLY
 __global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
                                                      int32_t *status, uint32_t first, uint32_t count, BlkInfo *info,
                                                      GroupRec *recs, uint32_t gmax, const uint32_t *order,
@@ -218,6 +219,7 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const ui
     }
     info[lin] = bi;
 }
+#endif  // QLZX_K2_ONLY
 
 // ------------------------------------------------------------------------------- K2 ----
 constexpr uint32_t kV4W = 4096;   // output window (LDS ring)

@@ -91,6 +91,7 @@ __device__ __forceinline__ uint32_t order_class(uint32_t len) {
     const uint32_t c = len >> 9;
     return c < kOrderClasses - 1 ? c : kOrderClasses - 1;
 }
+#ifndef QLZX_K2_ONLY
 __global__ void __launch_bounds__(kOrderWG) k_order_count(const uint32_t *src_len, uint32_t n, uint32_t *aux) {
     __shared__ uint32_t h[kOrderClasses];
     const uint32_t tid = threadIdx.x, i0 = blockIdx.x * kOrderPerWG + tid;
@@ -109,6 +110,8 @@ __global__ void __launch_bounds__(kOrderWG) k_order_count(const uint32_t *src_le
     for (uint32_t k = tid; k < kOrderClasses; k += kOrderWG)
         if (h[k]) atomicAdd(&aux[k], h[k]);
 }
+#endif  // QLZX_K2_ONLY
+#ifndef QLZX_K2_ONLY
 __global__ void __launch_bounds__(kOrderWG) k_order_scatter(const uint32_t *src_len, uint32_t n, uint32_t *aux,
                                                            uint32_t *list) {
     __shared__ uint32_t start[kOrderClasses], lc[kOrderClasses];
@@ -140,6 +143,7 @@ __global__ void __launch_bounds__(kOrderWG) k_order_scatter(const uint32_t *src_
     for (uint32_t e = 0; e < kOrderEPT; e++)
         if (i0 + e * kOrderWG < n) list[start[c[e]] + r[e]] = i0 + e * kOrderWG;
 }
+#endif  // QLZX_K2_ONLY
 
 // ------------------------------------------------------------------ K1 ----
 // Header checks of one block of `len` bytes (quicklz.c:780-811 and the batch API's bounds):
@@ -244,11 +248,14 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
 }
 
 }  // namespace qlzx
+#ifndef QLZX_K2_ONLY
 #include "qlzx_decode_solo.hip"
 #include "qlzx_decode_small.hip"
+#endif
 #include "qlzx_decode_v4.hip"
 namespace qlzx {
 
+#ifndef QLZX_K2_ONLY
 // Set by an atexit handler registered once the runtime is in use (after HIP registered its own
 // teardown; atexit runs in reverse order): per-thread HIP objects destroyed after that (threads
 // exiting during process exit) are left to the runtime's teardown.
@@ -258,6 +265,11 @@ inline void note_hip_up() {
     std::call_once(once, [] { std::atexit([] { g_hip_down.store(true); }); });
 }
 
+#if QLZX_SPLIT_K2  // K2 without CRC lives in qlzx_k2.hip (its own scheduler strategy)
+int launch_k2_nocrc(uint32_t grid, hipStream_t s, const qlzx_blocks &b, uint32_t *dsize, int32_t *status,
+                    uint32_t first, uint32_t cnt, const BlkInfo *info, const GroupRec *recs, uint32_t gmax,
+                    const uint32_t *order);
+#endif
 inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uint32_t *dsize,
                               int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
                               uint32_t *crc_out, uint32_t max_dsize, void *ws, size_t ws_bytes,
@@ -367,8 +379,12 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
             hipLaunchKernelGGL(k_dec_chunk4<true>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
                                recs, gmax, (const uint32_t *)order, crc_state, crc_expect, crc_out);
         else
+#if QLZX_SPLIT_K2
+            (void)launch_k2_nocrc(cnt, s, b, dsize, status, first, cnt, info, recs, gmax, (const uint32_t *)order);
+#else
             hipLaunchKernelGGL(k_dec_chunk4<false>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
                                recs, gmax, (const uint32_t *)order, nullptr, nullptr, nullptr);
+#endif
         if (overlap) (void)hipEventRecord(ev_k2[c & 1], s);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
@@ -376,4 +392,5 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     return 0;
 }
 
+#endif  // QLZX_K2_ONLY
 }  // namespace qlzx

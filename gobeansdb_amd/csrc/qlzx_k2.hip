@@ -1,0 +1,34 @@
+// qlzx_k2.hip -- K2 of the batch decoder without the CRC prologue (k_dec_chunk4<false>) in a
+// translation unit of its own, compiled with the iterative-ilp machine scheduler
+// (-mllvm -amdgpu-sched-strategy=iterative-ilp, gobeansdb_amd/build.py): that strategy speeds this
+// kernel up but slows K2 with its CRC prologue, the encoder and the replay kernels, and the
+// strategy is per translation unit (profiles/r05_sched_strategy_ab.txt).  Under QLZX_K2_ONLY the
+// shared sources define no other kernel.  The rest of the library is qlzx_api.hip.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <cstdlib>
+#include <mutex>
+
+#define QLZX_K2_ONLY 1
+#include "qlzx_device.h"
+namespace qlzx {  // defined in qlzx_tables.hip (qlzx_api.hip's unit); K2 without CRC reads none of them
+constexpr int kMulTabs = 7;
+extern __device__ uint32_t g_crc_mul[kMulTabs * 1024];
+extern __device__ uint32_t g_crc_mul32[1024];
+}  // namespace qlzx
+#include "qlzx_crc.hip"
+#include "qlzx_decode_wave.hip"
+
+namespace qlzx {
+
+int launch_k2_nocrc(uint32_t grid, hipStream_t s, const qlzx_blocks &b, uint32_t *dsize, int32_t *status,
+                    uint32_t first, uint32_t cnt, const BlkInfo *info, const GroupRec *recs, uint32_t gmax,
+                    const uint32_t *order) {
+    hipLaunchKernelGGL(k_dec_chunk4<false>, dim3(grid), dim3(64), 0, s, b, dsize, status, first, cnt, info, recs,
+                       gmax, order, nullptr, nullptr, nullptr);
+    return (int)hipGetLastError();
+}
+
+}  // namespace qlzx

@@ -21,15 +21,28 @@ def test_library_builds_and_exports_header_symbols():
 
 
 def test_gfx950_code_object_present(tmp_path):
-    # the fat binary (.hip_fatbin, a zstd-compressed offload bundle since round 5) carries a
-    # gfx950 code object: list the bundle's entries with the ROCm LLVM tools
+    # the fat binary section (.hip_fatbin) holds one zstd-compressed offload bundle ("CCOB") per
+    # translation unit (qlzx_api.hip and qlzx_k2.hip since round 5): each carries a gfx950 code
+    # object -- list every bundle's entries with the ROCm LLVM tools
+    import re
     bin_dir = "/opt/rocm/lib/llvm/bin"
     fb = tmp_path / "fatbin.bin"
     subprocess.run([f"{bin_dir}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", _lib.LIB_PATH,
                     str(tmp_path / "host.o")], check=True)
-    out = subprocess.run([f"{bin_dir}/clang-offload-bundler", "--list", "--type=o", f"--input={fb}"],
-                         capture_output=True, text=True, check=True).stdout
-    assert "hipv4-amdgcn-amd-amdhsa--gfx950" in out.split()
+    data = fb.read_bytes()
+    starts = [m.start() for m in re.finditer(b"CCOB|__CLANG_OFFLOAD_BUNDLE__", data)]
+    assert starts and starts[0] == 0
+    import struct
+    for a, b in zip(starts, starts[1:] + [len(data)]):
+        end = b
+        if data[a:a + 4] == b"CCOB":  # compressed bundle: its header holds its total size (v3: u64, v2: u32)
+            ver = struct.unpack_from("<H", data, a + 4)[0]
+            end = a + (struct.unpack_from("<Q", data, a + 8)[0] if ver >= 3 else struct.unpack_from("<I", data, a + 8)[0])
+        part = tmp_path / f"bundle_{a}.bin"
+        part.write_bytes(data[a:end])
+        out = subprocess.run([f"{bin_dir}/clang-offload-bundler", "--list", "--type=o", f"--input={part}"],
+                             capture_output=True, text=True, check=True).stdout
+        assert "hipv4-amdgcn-amd-amdhsa--gfx950" in out.split(), (a, out)
 
 
 def test_settings_match_reference(golden):
