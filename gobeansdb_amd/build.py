@@ -44,8 +44,9 @@ def _stale() -> bool:
 PROF_OUT = os.path.join(HERE, "libqlzx_prof.so")
 
 
-# K2 without its CRC prologue (k_dec_chunk4<false>) is compiled in a translation unit of its own
-# with this machine-scheduler strategy (csrc/qlzx_k2.hip; profiles/r05_sched_strategy_ab.txt)
+# K1 (k_dec_parse6) and K2 without its CRC prologue (k_dec_chunk4<false>) are compiled in a
+# translation unit of their own with this machine-scheduler strategy (csrc/qlzx_k2.hip;
+# profiles/r05_sched_strategy_ab.txt)
 K2_SCHED = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 
 
@@ -65,8 +66,10 @@ def _compile(out: str, extra: list[str], verbose: bool, split: bool = True) -> N
         _run([*base, "-shared", *api, "-o", out + ".tmp", os.path.join(CSRC, "qlzx_api.hip")], verbose)
     else:
         oa, ok2 = out + ".api.o", out + ".k2.o"
-        _run([*base, "-c", *api, "-DQLZX_SPLIT_K2=1", "-o", oa, os.path.join(CSRC, "qlzx_api.hip")], verbose)
-        _run([*base, "-c", *extra, *K2_SCHED, "-o", ok2, os.path.join(CSRC, "qlzx_k2.hip")], verbose)
+        _run([*base, "-c", *api, "-DQLZX_SPLIT_K2=1", "-DQLZX_SPLIT_K1=1", "-o", oa, os.path.join(CSRC, "qlzx_api.hip")],
+             verbose)
+        _run([*base, "-c", "-DQLZX_SPLIT_K1=1", *extra, *K2_SCHED, "-o", ok2, os.path.join(CSRC, "qlzx_k2.hip")],
+             verbose)
         _run(["hipcc", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", out + ".tmp", oa, ok2], verbose)
         for f in (oa, ok2):
             os.remove(f)

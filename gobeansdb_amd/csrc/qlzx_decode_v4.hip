@@ -22,6 +22,9 @@
 //     token dword, so no prefetched register is copied (and waited for) at a batch boundary.
 //
 // Checks C1-C5 are applied exactly as by the oracle (oracle/qlz_oracle.c:180-231).
+#ifndef QLZX_SPLIT_K1  // 1 (release build): K1 lives in qlzx_k2.hip's unit, launched through launch_k1_parse6
+#define QLZX_SPLIT_K1 0
+#endif
 namespace qlzx {
 
 // ------------------------------------------------------------------------------- K1 ----
@@ -34,7 +37,7 @@ namespace qlzx {
 // round.  Here lanes drift apart in stream position and the wave pays kmax steps per iteration.
 // c2 25.1-25.3 -> 24.7-24.9 ms at kmax 16; c4 346 -> 377 GiB/s at kmax 10
 // (tools/gpu_r5lr3.sh, profiles/r05_k1_lane_ring_ab.txt).
-#ifndef QLZX_K2_ONLY
+#if (!defined(QLZX_K2_ONLY) && !QLZX_SPLIT_K1) || (defined(QLZX_K2_ONLY) && QLZX_SPLIT_K1)
 __global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
                                                      int32_t *status, uint32_t first, uint32_t count, BlkInfo *info,
                                                      GroupRec *recs, uint32_t gmax, const uint32_t *order,

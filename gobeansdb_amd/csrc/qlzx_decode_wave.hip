@@ -265,6 +265,11 @@ inline void note_hip_up() {
     std::call_once(once, [] { std::atexit([] { g_hip_down.store(true); }); });
 }
 
+#if QLZX_SPLIT_K1
+int launch_k1_parse6(uint32_t grid, hipStream_t s, const qlzx_blocks &b, const uint32_t *dst_cap, uint32_t *dsize,
+                     int32_t *status, uint32_t first, uint32_t cnt, BlkInfo *info, GroupRec *recs, uint32_t gmax,
+                     const uint32_t *order, uint32_t max_dsize, uint32_t kmax);
+#endif
 #if QLZX_SPLIT_K2  // K2 without CRC lives in qlzx_k2.hip (its own scheduler strategy)
 int launch_k2_nocrc(uint32_t grid, hipStream_t s, const qlzx_blocks &b, uint32_t *dsize, int32_t *status,
                     uint32_t first, uint32_t cnt, const BlkInfo *info, const GroupRec *recs, uint32_t gmax,
@@ -371,8 +376,13 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         if (overlap && c >= 2) (void)hipStreamWaitEvent(s1, ev_k2[c & 1], 0);  // K2(c-2) freed this half
         // K1's step budget per iteration: 16 for uniform 16 KiB calls, 10 for mixed sizes (c4:
         // 377 vs 363 GiB/s; c5 580 vs 560)
+#if QLZX_SPLIT_K1
+        (void)launch_k1_parse6((cnt + kParseWG - 1) / kParseWG, s1, b, dst_cap, dsize, status, first, cnt, info, recs,
+                               gmax, order, max_dsize, max_dsize > 16384 ? 10u : 16u);
+#else
         hipLaunchKernelGGL(k_dec_parse6, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b, dst_cap, dsize,
                            status, first, cnt, info, recs, gmax, order, max_dsize, max_dsize > 16384 ? 10u : 16u);
+#endif
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], s1), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
         // one kernel for every block size: the LDS window slides over longer blocks
         if (crc)
