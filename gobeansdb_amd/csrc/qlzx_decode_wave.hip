@@ -265,6 +265,13 @@ inline void note_hip_up() {
     std::call_once(once, [] { std::atexit([] { g_hip_down.store(true); }); });
 }
 
+#ifndef QLZX_K1_KMAX_UNI  // K1's step budget per iteration: uniform 16 KiB calls / mixed sizes (16 / 10 with the
+                          // default scheduler; 12 / 10 under iterative-ILP: profiles/r05_sched_strategy_ab.txt)
+#define QLZX_K1_KMAX_UNI 12
+#endif
+#ifndef QLZX_K1_KMAX_MIX
+#define QLZX_K1_KMAX_MIX 10
+#endif
 #if QLZX_SPLIT_K1
 int launch_k1_parse6(uint32_t grid, hipStream_t s, const qlzx_blocks &b, const uint32_t *dst_cap, uint32_t *dsize,
                      int32_t *status, uint32_t first, uint32_t cnt, BlkInfo *info, GroupRec *recs, uint32_t gmax,
@@ -378,10 +385,10 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         // 377 vs 363 GiB/s; c5 580 vs 560)
 #if QLZX_SPLIT_K1
         (void)launch_k1_parse6((cnt + kParseWG - 1) / kParseWG, s1, b, dst_cap, dsize, status, first, cnt, info, recs,
-                               gmax, order, max_dsize, max_dsize > 16384 ? 10u : 16u);
+                               gmax, order, max_dsize, max_dsize > 16384 ? (uint32_t)QLZX_K1_KMAX_MIX : (uint32_t)QLZX_K1_KMAX_UNI);
 #else
         hipLaunchKernelGGL(k_dec_parse6, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b, dst_cap, dsize,
-                           status, first, cnt, info, recs, gmax, order, max_dsize, max_dsize > 16384 ? 10u : 16u);
+                           status, first, cnt, info, recs, gmax, order, max_dsize, max_dsize > 16384 ? (uint32_t)QLZX_K1_KMAX_MIX : (uint32_t)QLZX_K1_KMAX_UNI);
 #endif
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], s1), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
         // one kernel for every block size: the LDS window slides over longer blocks
