@@ -15,10 +15,14 @@ ARCH = os.environ.get("QLZX_ARCH", "gfx950")
 
 
 def source_hash() -> str:
-    """sha256 (first 16 hex digits) of every csrc/* file and include/qlzx.h, by name and content:
-    compiled into the library (qlzx_info: "src <hash>"), so a binary is tied to the sources."""
+    """sha256 (first 16 hex digits) of every csrc/* file, include/qlzx.h and this build script
+    (its compile flags, scheduler strategy and split layout), by name and content, plus the target
+    arch: compiled into the library (qlzx_info: "src <hash>"), so a binary is tied to the sources
+    and the way they were compiled."""
     h = hashlib.sha256()
-    srcs = sorted(glob.glob(os.path.join(CSRC, "*"))) + [os.path.join(ROOT, "include", "qlzx.h")]
+    h.update(("arch=" + ARCH + "\0").encode())
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*"))) + [os.path.join(ROOT, "include", "qlzx.h"),
+                                                         os.path.abspath(__file__)]
     for s in srcs:
         if os.path.isfile(s):
             h.update(os.path.relpath(s, ROOT).encode() + b"\0")

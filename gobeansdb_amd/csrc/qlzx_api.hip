@@ -825,6 +825,13 @@ extern "C" {
 int qlzx_last_status(void) { return t_last_status; }
 
 int qlzx_service_test_fault(int mode) {
+    // a test hook: armed only in a process started with QLZX_TEST_HOOKS=1 (read once), so no
+    // caller of the release library can make another thread's drop-in call fail
+    static const bool armed = [] {
+        const char *e = std::getenv("QLZX_TEST_HOOKS");
+        return e && e[0] == '1';
+    }();
+    if (!armed) return fail(QLZX_R_BAD_ARG, "qlzx_service_test_fault: test hooks are off (QLZX_TEST_HOOKS=1)");
     if (mode != 1 && mode != 2) return fail(QLZX_R_BAD_ARG, "qlzx_service_test_fault: mode is 1 or 2");
     Service *S = service();
     if (!S) return QLZX_R_NO_DEVICE;

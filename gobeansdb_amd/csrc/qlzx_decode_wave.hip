@@ -381,11 +381,13 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
         hipStream_t s1 = overlap ? (split_k1 && (c & 1) ? side2 : side) : s;
         if (overlap && c >= 2) (void)hipStreamWaitEvent(s1, ev_k2[c & 1], 0);  // K2(c-2) freed this half
-        // K1's step budget per iteration: 16 for uniform 16 KiB calls, 10 for mixed sizes (c4:
-        // 377 vs 363 GiB/s; c5 580 vs 560)
+        // K1's step budget per iteration: QLZX_K1_KMAX_UNI (12) for uniform 16 KiB calls,
+        // QLZX_K1_KMAX_MIX (10) for mixed sizes (c4: 377 vs 363 GiB/s; c5 580 vs 560)
 #if QLZX_SPLIT_K1
-        (void)launch_k1_parse6((cnt + kParseWG - 1) / kParseWG, s1, b, dst_cap, dsize, status, first, cnt, info, recs,
-                               gmax, order, max_dsize, max_dsize > 16384 ? (uint32_t)QLZX_K1_KMAX_MIX : (uint32_t)QLZX_K1_KMAX_UNI);
+        // the helpers return hipGetLastError(), which also clears the error: keep it here
+        if (const int e1 = launch_k1_parse6((cnt + kParseWG - 1) / kParseWG, s1, b, dst_cap, dsize, status, first, cnt, info, recs,
+                               gmax, order, max_dsize, max_dsize > 16384 ? (uint32_t)QLZX_K1_KMAX_MIX : (uint32_t)QLZX_K1_KMAX_UNI))
+            return e1;
 #else
         hipLaunchKernelGGL(k_dec_parse6, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b, dst_cap, dsize,
                            status, first, cnt, info, recs, gmax, order, max_dsize, max_dsize > 16384 ? (uint32_t)QLZX_K1_KMAX_MIX : (uint32_t)QLZX_K1_KMAX_UNI);
@@ -397,7 +399,9 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
                                recs, gmax, (const uint32_t *)order, crc_state, crc_expect, crc_out);
         else
 #if QLZX_SPLIT_K2
-            (void)launch_k2_nocrc(cnt, s, b, dsize, status, first, cnt, info, recs, gmax, (const uint32_t *)order);
+            if (const int e2 = launch_k2_nocrc(cnt, s, b, dsize, status, first, cnt, info, recs, gmax,
+                                               (const uint32_t *)order))
+                return e2;
 #else
             hipLaunchKernelGGL(k_dec_chunk4<false>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
                                recs, gmax, (const uint32_t *)order, nullptr, nullptr, nullptr);

@@ -359,13 +359,17 @@ struct Service {
                     }
                     const int lr = batch.empty() ? QLZX_R_OK : launch(batch);
                     if (lr != QLZX_R_OK) {
+                        bool mine = false;  // the leader's own request may belong to an earlier batch
                         for (const auto &p : batch) {
                             volatile qlzx::SvcDone *x = h_done + p.r.slot;
                             x->status = -1;
                             x->seq = p.r.seq;
                             slot_ev[p.r.slot].store(tag(p.r.seq, kNoEv), std::memory_order_release);
+                            mine = mine || (p.r.slot == r.slot && p.r.seq == r.seq);
                         }
-                        rc = lr;
+                        // only the failed batch's requests fail: one of an earlier, still running
+                        // batch completes normally (the status -1 / kNoEv tags above fail the rest)
+                        if (mine) rc = lr;
                     }
                     leading.store(false, std::memory_order_release);
                     continue;

@@ -137,9 +137,11 @@ def Decompress(source) -> bytes:
     if level == 3 and (s[0] & 1):
         # qlz_decompress reads SizeCompressed(s) bytes (quicklz.c:777-836 trusts the header);
         # Go never reads that field: it decodes any stream whose tokens fit in len(source) and
-        # panics on the first index past it (quicklz.go:291-431).  A header csize above len(s)
-        # is therefore rewritten to len(s): the decoder is then bounded exactly where Go is.
-        if len(s) < SizeCompressed(s):
+        # panics on the first index past it (quicklz.go:291-431).  A header csize that differs
+        # from len(s), above or below, is therefore rewritten to len(s): the decoder is bounded
+        # by the bytes Go may index.  Known difference: Go ignores bytes after the item that
+        # completes dsize, while check C5 rejects a stream with such trailing bytes.
+        if len(s) != SizeCompressed(s):
             b = bytearray(s)
             if s[0] & 2:
                 b[1:5] = len(s).to_bytes(4, "little")

@@ -250,7 +250,9 @@ const char *qlzx_last_error(void);
 /* Library/version info: fills `buf` with a short description (arch, kernels, source hash). */
 int qlzx_info(char *buf, size_t len);
 
-/* Test hook for the request path behind the drop-ins (values <= 64 KiB): the next batch the
+/* INTERNAL test hook, inert unless the process was started with QLZX_TEST_HOOKS=1 (read once;
+ * otherwise it returns QLZX_R_BAD_ARG and changes nothing).
+ * For the request path behind the drop-ins (values <= 64 KiB): the next batch the
  * current device's service launches fails -- mode 1: its kernel runs but publishes no
  * completion (caught through the batch event), mode 2: the launch itself fails.  Every request
  * of that batch then fails with QLZX_R_HIP (qlzx_compress1 returns 0, the quicklz.h drop-ins

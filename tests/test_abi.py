@@ -90,3 +90,17 @@ def test_drop_ins_fail_stop_without_a_device():
         assert p.returncode != 0, (call, p.stdout, p.stderr)
         assert "returned" not in p.stdout
         assert "libqlzx:" in p.stderr and "no error channel" in p.stderr, p.stderr
+
+
+def test_service_test_hook_is_inert_by_default():
+    """qlzx_service_test_fault is a test hook: without QLZX_TEST_HOOKS=1 in the process
+    environment it refuses (QLZX_R_BAD_ARG = -1) before touching the request service, so no caller
+    of the release library can make another thread's drop-in call fail."""
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from gobeansdb_amd import _lib; "
+            "L = _lib.lib(); print('rc', L.qlzx_service_test_fault(1)); "
+            "print('err', L.qlzx_last_error().decode())") % (os.path.dirname(os.path.dirname(__file__)),)
+    env = {k: v for k, v in os.environ.items() if k != "QLZX_TEST_HOOKS"}
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert "rc -1" in p.stdout and "test hooks are off" in p.stdout, p.stdout

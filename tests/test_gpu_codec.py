@@ -378,3 +378,23 @@ def test_decompress_inflated_header_csize_decodes_like_go(cuda):
         cut = inflated[:len(c) - 7]  # tokens run past the buffer: Go panics
         with pytest.raises(QuicklzError):
             Decompress(cut)
+
+
+def test_decompress_deflated_header_csize_decodes_like_go(cuda):
+    """The other direction: a valid stream whose header csize is SMALLER than the
+    buffer its tokens use.  Go never reads the field, so it decodes; the mirror rewrites csize to
+    len(s) and decodes the same bytes.  A stream with bytes after its last item is the one
+    documented difference (check C5 rejects it; Go ignores them)."""
+    import struct
+    from gobeansdb_amd.quicklz import Decompress, QuicklzError
+    for n in (100, 5000, 70000):
+        v = O.gen_text(37, n, n)
+        c = O.compress(v)
+        assert c[0] & 1
+        if c[0] & 2:
+            small = c[:1] + struct.pack("<I", len(c) - 5) + c[5:]
+        else:
+            small = c[:1] + bytes([len(c) - 5]) + c[2:]
+        assert Decompress(small) == v
+        with pytest.raises(QuicklzError):
+            Decompress(c + b"\0\0\0")  # trailing bytes after the last item: C5

@@ -7,7 +7,11 @@ values of many sizes and kinds, and every result must equal the oracle's: a slot
 index mixed up between callers would show as another caller's bytes.
 """
 import ctypes
+import os
 import threading
+
+# arms qlzx_service_test_fault (read once by the library, at its first call)
+os.environ.setdefault("QLZX_TEST_HOOKS", "1")
 
 import numpy as np
 import pytest
