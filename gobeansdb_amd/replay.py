@@ -183,3 +183,223 @@ def _vhash(src: torch.Tensor, off: torch.Tensor, length: torch.Tensor, out16: to
     rc = L.qlzx_vhash_batch(src.data_ptr(), o.data_ptr(), ln.data_ptr(), n, tmp.data_ptr(), batch._stream(stream))
     _lib.check(rc, "qlzx_vhash_batch")
     out16[where] = tmp
+
+
+@dataclass
+class HostReplayPart:
+    """What the pipelined replay of one part leaves in host (pinned) memory.
+
+    want="values": the per-record fields a reader of the values needs (offset, stored header,
+    flag and length after Payload.Decompress, in_out / val_off, vhash) and the decoder's output
+    buffer; a value with in_out 0 is the part's own bytes at val_off (the host already holds them).
+    want="hints": buildHintFromData's fields only (store/bucket.go:89-117: the decompressed body
+    only feeds Getvhash and is freed): offset, stored header, vhash."""
+    n: int
+    end_error: bool
+    offset: torch.Tensor
+    header: torch.Tensor
+    vhash: torch.Tensor
+    flag: torch.Tensor | None = None
+    value_len: torch.Tensor | None = None
+    in_out: torch.Tensor | None = None
+    val_off: torch.Tensor | None = None
+    values: torch.Tensor | None = None
+
+    def value(self, part: torch.Tensor | np.ndarray, j: int) -> memoryview:
+        """Record j's value after Payload.Decompress, from host memory (the decoder output copied
+        back, or the part itself)."""
+        o, n = int(self.val_off[j]), int(self.value_len[j])
+        src = self.values if int(self.in_out[j]) else part
+        a = src.numpy() if isinstance(src, torch.Tensor) else src
+        return memoryview(a)[o:o + n]
+
+
+class ReplayPipeline:
+    """Replay of .data streams held in pinned host memory (chunk files read from disk),
+    pipelined over three streams: pinned H2D of part i+1 || replay of part i || pinned D2H of
+    part i-1's results (PCIe is full duplex), two device slots for the parts.  The streams, slots
+    and host buffers are made once, here, for parts of at most `part_cap` bytes; run() then moves
+    no allocation into the copy/replay loop (a host buffer only grows when a part needs more).
+
+    want="values": the decompressed values and their per-record fields go back into two pinned
+    host slots (`values_cap` bytes of decoder output each to start with), reused every other part.
+    want="hints": buildHintFromData's fields only, into `nparts` per-part pinned buffers."""
+
+    def __init__(self, part_cap: int, want: str = "values", device=None, workspace: batch.Workspace | None = None,
+                 values_cap: int = 0, nparts: int = 0):
+        if want not in ("values", "hints"):
+            raise ValueError("want is 'values' or 'hints'")
+        self.want = want
+        self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.ws = workspace or batch.Workspace(self.dev)
+        self.part_cap = max(int(part_cap), 1)
+        self.s_h2d, self.s_cmp, self.s_d2h = (torch.cuda.Stream(self.dev) for _ in range(3))
+        self.dslot = [torch.empty(self.part_cap, dtype=torch.uint8, device=self.dev) for _ in range(2)]
+        self.ev_in = [torch.cuda.Event(), torch.cuda.Event()]      # part landed in its device slot
+        self.ev_used = [torch.cuda.Event(), torch.cuda.Event()]    # replay done with the device slot
+        self.ev_out = [torch.cuda.Event(), torch.cuda.Event()]     # D2H into the host slot done
+        rec_cap = self.part_cap // 256 + 1                         # records are 256-B aligned
+        if want == "values":
+            self.host = [self._values_slot(rec_cap, values_cap) for _ in range(2)]
+        else:
+            self.host = [self._hint_slot(rec_cap) for _ in range(max(nparts, 0))]
+
+    @staticmethod
+    def _pinned(n, dtype, shape=None):
+        return torch.empty(shape if shape is not None else max(n, 1), dtype=dtype).pin_memory()
+
+    def _values_slot(self, recs, nbytes):
+        p = self._pinned
+        return dict(cap=recs, values=p(nbytes, torch.uint8), off=p(recs, torch.int64),
+                    hdr=p(0, torch.int32, (recs, 6)), vh=p(recs, torch.int32), flag=p(recs, torch.int32),
+                    vlen=p(recs, torch.int32), io=p(recs, torch.uint8), voff=p(recs, torch.int64))
+
+    def _hint_slot(self, recs):
+        p = self._pinned
+        return dict(cap=recs, off=p(recs, torch.int64), hdr=p(0, torch.int32, (recs, 6)), vh=p(recs, torch.int32))
+
+    def run(self, parts: list[torch.Tensor], sink=None) -> list["HostReplayPart | None"]:
+        """Replay every part (each a whole .data stream cut at record starts, in pinned memory).
+        want="values": `sink(i, HostReplayPart)` (optional) runs once part i's copy has landed and
+        before its host slot is reused (the host waits for it: a checking pass); without a sink
+        nothing waits, and only the last two parts' results are left valid in the returned list
+        (the others are None).  want="hints": every part's result is returned (and passed to
+        `sink` at the end if given)."""
+        np_ = len(parts)
+        out: list[HostReplayPart | None] = [None] * np_
+        if np_ == 0:
+            return out
+        if any(int(q.numel()) > self.part_cap for q in parts):
+            raise ValueError("a part is larger than the pipeline's part_cap")
+        if self.want == "hints":
+            while len(self.host) < np_:
+                self.host.append(self._hint_slot(self.part_cap // 256 + 1))
+        s_h2d, s_cmp, s_d2h = self.s_h2d, self.s_cmp, self.s_d2h
+        dslot, ev_in, ev_used, ev_out = self.dslot, self.ev_in, self.ev_used, self.ev_out
+        pend: list[int | None] = [None, None]   # part whose results a host slot holds (sink not run yet)
+
+        def h2d(i):
+            dslot[i & 1][: parts[i].numel()].copy_(parts[i], non_blocking=True)
+            ev_in[i & 1].record(s_h2d)
+
+        def flush(j):
+            i = pend[j]
+            if i is not None:
+                ev_out[j].synchronize()
+                sink(i, out[i])
+                pend[j] = None
+
+        with torch.cuda.stream(s_h2d):
+            h2d(0)
+        for i in range(np_):
+            j = i & 1
+            if i + 1 < np_:   # prefetch the next part while this one replays
+                with torch.cuda.stream(s_h2d):
+                    if i >= 1:
+                        s_h2d.wait_event(ev_used[j ^ 1])
+                    h2d(i + 1)
+            with torch.cuda.stream(s_cmp):
+                s_cmp.wait_event(ev_in[j])
+                r = replay(dslot[j][: parts[i].numel()], workspace=self.ws, stream=s_cmp)
+                ev_used[j].record(s_cmp)
+            n = r.n
+            if self.want == "hints":
+                h = self.host[i]
+                hp = HostReplayPart(n, r.end_error, h["off"][:n], h["hdr"][:n], h["vh"][:n])
+            else:
+                if sink is not None:
+                    flush(j)
+                nb = int(r.values.data.numel())
+                h = self.host[j]
+                if h["cap"] < n or h["values"].numel() < nb:   # grow (a copy may still target the old one)
+                    ev_out[j].synchronize()
+                    h = self.host[j] = self._values_slot(max(n, h["cap"]), max(nb, h["values"].numel()))
+                hp = HostReplayPart(n, r.end_error, h["off"][:n], h["hdr"][:n], h["vh"][:n], h["flag"][:n],
+                                    h["vlen"][:n], h["io"][:n], h["voff"][:n], h["values"][:nb])
+                if i >= 2 and sink is None:
+                    out[i - 2] = None   # its host slot is reused now
+            with torch.cuda.stream(s_d2h):
+                s_d2h.wait_event(ev_used[j])
+                if i >= 2:
+                    s_d2h.wait_event(ev_out[j])
+                srcs = [(hp.offset, r.offset), (hp.header, r.header), (hp.vhash, r.vhash)]
+                if self.want == "values":
+                    srcs += [(hp.flag, r.flag), (hp.value_len, r.value_len), (hp.in_out, r.in_out),
+                             (hp.val_off, r.val_off), (hp.values, r.values.data)]
+                for dst, src in srcs:
+                    if src.numel():
+                        dst.copy_(src, non_blocking=True)
+                        src.record_stream(s_d2h)
+                ev_out[j].record(s_d2h)
+            out[i] = hp
+            if self.want == "values" and sink is not None:
+                pend[j] = i
+        if self.want == "values" and sink is not None:
+            for j in (((np_ - 2) & 1, (np_ - 1) & 1) if np_ >= 2 else (0,)):
+                flush(j)
+        for e in ev_out:
+            e.synchronize()
+        if self.want == "hints" and sink is not None:
+            for i, hp in enumerate(out):
+                sink(i, hp)
+        return out
+
+
+def replay_pipelined(parts: list[torch.Tensor], want: str = "values", device=None,
+                     workspace: batch.Workspace | None = None, sink=None) -> list["HostReplayPart | None"]:
+    """One-shot ReplayPipeline(max part size, want).run(parts, sink)."""
+    cap = max([int(q.numel()) for q in parts], default=1)
+    return ReplayPipeline(cap, want, device, workspace, nparts=len(parts)).run(parts, sink)
+
+
+def host_value_digest(hp: HostReplayPart, part, key_base: int = 0, file_id: int = 0, threads: int = 16) -> int:
+    """XOR over the part's records of crc32 (zlib's = store/crc32.go's) of each value as it sits
+    in HOST memory after the pipelined replay, keyed by the record's place like the device-only
+    digest: crc ^ ((key_base + offset) * 0x85EBCA77 + (file_id + 1) * 0x9E3779B1) mod 2^32."""
+    import zlib
+    from concurrent.futures import ThreadPoolExecutor
+    n = hp.n
+    if n == 0:
+        return 0
+    off = hp.offset.numpy()
+    voff = hp.val_off.numpy()
+    vlen = hp.value_len.numpy()
+    io = hp.in_out.numpy()
+    pa = part.numpy() if isinstance(part, torch.Tensor) else np.asarray(part)
+    vals = memoryview(hp.values.numpy())
+    raw = memoryview(pa)
+    keys = ((key_base + off.astype(np.int64)) * 0x85EBCA77 + (file_id + 1) * 0x9E3779B1) & 0xFFFFFFFF
+
+    def run(lo, hi):
+        d = 0
+        for j in range(lo, hi):
+            o = int(voff[j])
+            src = vals if io[j] else raw
+            d ^= zlib.crc32(src[o:o + int(vlen[j])]) ^ int(keys[j])
+        return d
+
+    t = max(1, min(threads, n // 256 + 1))
+    cuts = [n * k // t for k in range(t + 1)]
+    with ThreadPoolExecutor(t) as ex:
+        parts_ = list(ex.map(lambda k: run(cuts[k], cuts[k + 1]), range(t)))
+    d = 0
+    for x in parts_:
+        d ^= x
+    return d
+
+
+def hint_digest(offset, header, vhash, key_base: int = 0, file_id: int = 0) -> int:
+    """XOR over records of a keyed mix of the hint fields (offset, stored header, vhash): the
+    parity digest of buildHintFromData's output; torch tensors (host or device) or arrays."""
+    def a(x):
+        return x.cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
+    off = a(offset).astype(np.int64) + key_base
+    hdr = a(header).astype(np.int64).reshape(-1, 6) & 0xFFFFFFFF
+    vh = a(vhash).astype(np.int64) & 0xFFFF
+    if off.size == 0:
+        return 0
+    m = (off * 0x85EBCA77 + (file_id + 1) * 0x9E3779B1) & 0xFFFFFFFF
+    for c in range(6):
+        m = (m * 0x01000193 ^ hdr[:, c]) & 0xFFFFFFFF
+    m = (m * 0x01000193 ^ vh) & 0xFFFFFFFF
+    return int(np.bitwise_xor.reduce(m))

@@ -71,3 +71,13 @@ def test_truncated_and_partial_tail():
     # garbage slot (invalid ksz) then a record: nextValid skips it
     recs, err = R.stream_all(a + bytes(256) + b)
     assert [(r.offset, r.size_broken) for r in recs] == [(0, 0), (512, 256)] and err is None
+
+
+def test_fnv1a_reference_kat():
+    """store/htree_test.go:18-23 (TestHash): utils.Fnv1a([]byte("test")) == 2949673445."""
+    assert R.fnv1a(b"test") == 2949673445
+    # bytes >= 0x80 are sign-extended (utils/hash.go:12, h ^= uint32(int8(b))): differs from FNV-1a
+    plain = 0x811C9DC5
+    for b in b"\xff":
+        plain = ((plain ^ b) * 0x01000193) & 0xFFFFFFFF
+    assert R.fnv1a(b"\xff") != plain

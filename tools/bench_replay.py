@@ -115,6 +115,16 @@ def build_chunk(mib: int, seed: int, dev):
     return buf, nrec, int(sum(len(v) for v in values[:nrec])), int(sum(sizes[:nrec])), np.asarray(rec_off, np.uint64)
 
 
+def _value_digest(res, lo: int, f: int) -> int:
+    """Device-only parity digest of one replayed piece: XOR over its records of crc32 of the value
+    after Payload.Decompress, keyed by the record's place (file f, offset lo + offset) since the
+    corpus repeats its two chunk files (a repeated record must not cancel itself out)."""
+    from gobeansdb_amd import shard
+    pos = res.offset.to(torch.int64) + lo
+    key = (pos * 0x85EBCA77 + (f + 1) * 0x9E3779B1) & 0xFFFFFFFF
+    return shard.xor_of((res.value_crcs().to(torch.int64) & 0xFFFFFFFF) ^ key)
+
+
 def pin_sample(c, res, k: int) -> int:
     """Full-size parity: every record offset against the chunk's layout, and k sampled records
     (offset, flag after Payload.Decompress, value bytes, Getvhash) against the oracle's
@@ -196,9 +206,12 @@ def run(a, rank: int, world: int, dev):
       once: its record count, no resync, and the XOR of its value CRCs (all-gathered into the
       corpus digest, the same at every N);
     * device-only: the rank's pieces from the resident chunks, a.steps passes;
-    * end to end: the same pieces pipelined from pinned host memory (H2D of piece i+1, replay of
-      piece i, D2H of piece i-1's decompressed values on three streams), and again with only the
-      hint fields going back (buildHintFromData frees each body after Getvhash).
+    * end to end (replay.replay_pipelined): the same pieces in parts pipelined from pinned host
+      memory (H2D of part i+1, replay of part i, D2H of part i-1's decompressed values and
+      per-record fields on three streams), and again with only the hint fields going back
+      (buildHintFromData frees each body after Getvhash).  Checked: an untimed pass of the values
+      pipeline CRCs every value in host memory (zlib) against the device-only digest, the timed
+      pass's last two parts likewise, and every part of the timed hints pass by a hint digest.
     Returns the record on rank 0 (max-over-ranks times, summed bytes; CPU leg at N = 1 only)."""
     from gobeansdb_amd import replay, batch, shard
     t0 = time.time()
@@ -229,7 +242,7 @@ def run(a, rank: int, world: int, dev):
     corpus = [f & 1 for f in range(a.files)]
     plan = shard.partition_data_files([(chunks[k]["rec_off"], len(chunks[k]["host"])) for k in corpus], world)
     pieces = [(corpus[f], lo, hi) for f, lo, hi in plan[rank]]
-    digest, nrec_mine, out_mine, out_cap = 0, 0, 0, 0
+    digest, hdigest, nrec_mine, out_mine, out_cap = 0, 0, 0, 0, 0
     for f, lo, hi in plan[rank]:
         c = chunks[corpus[f]]
         ro = c["rec_off"].astype(np.int64)
@@ -237,15 +250,13 @@ def run(a, rank: int, world: int, dev):
         res = replay.replay(c["dev"][lo:hi], workspace=ws)
         torch.cuda.synchronize()
         assert res.n == want and not res.end_error and int(res.size_broken.abs().sum()) == 0, (res.n, want)
-        # the corpus repeats its two chunk files, so each record's CRC is keyed by its place
-        # (file, offset) before the XOR: a repeated record does not cancel itself out
-        pos = res.offset.to(torch.int64) + lo
-        key = (pos * 0x85EBCA77 + (f + 1) * 0x9E3779B1) & 0xFFFFFFFF
-        digest ^= shard.xor_of((res.value_crcs().to(torch.int64) & 0xFFFFFFFF) ^ key)
+        digest ^= _value_digest(res, lo, f)
+        hdigest ^= replay.hint_digest(res.offset, res.header, res.vhash, lo, f)
         nrec_mine += res.n
         out_mine += int(res.value_len.to(torch.int64).sum())
-        out_cap = max(out_cap, res.values.data.numel())
+        out_cap = max(out_cap, int(res.values.data.numel()))
         del res
+    digest_mine = digest
     digest = shard.xor_digest_over_ranks(digest, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -272,14 +283,14 @@ def run(a, rank: int, world: int, dev):
     dev_ev = e0.elapsed_time(e1) * 1e-3
     share = sum(hi - lo for _, lo, hi in pieces)
 
-    # ---- end to end, pipelined: H2D of piece i+1 || replay of piece i || D2H of piece i-1 ----
-    # three streams, two device slots and two pinned output slots (PCIe is full duplex); only
-    # decompressed values travel back (raw values are bytes the host already holds)
-    # the end-to-end legs move each piece in parts of about --pipe-mib, cut at record starts
-    # (every record start of the generated chunks is a cut point; a part is a .data stream of its own)
-    parts = []
+    # ---- end to end from pinned host memory (replay.replay_pipelined): H2D of part i+1 ||
+    # replay of part i || D2H of part i-1's results, three streams.  The pieces move in parts of
+    # about --pipe-mib cut at record starts (every record start of the generated chunks is a cut
+    # point; a part is a .data stream of its own) ----
+    parts = []   # (file, chunk, lo, hi)
     step_b = max(getattr(a, "pipe_mib", 4096), 1) << 20
-    for k, lo, hi in pieces:
+    for f, lo, hi in plan[rank]:
+        k = corpus[f]
         ro = chunks[k]["rec_off"].astype(np.int64)
         x = lo
         while x < hi:
@@ -287,87 +298,73 @@ def run(a, rank: int, world: int, dev):
             idx = int(np.searchsorted(ro, want, side="left"))  # first record start at or past want
             y = int(ro[idx]) if want < hi and idx < len(ro) else hi
             y = min(y, hi)
-            parts.append((k, x, y))
+            parts.append((f, k, x, y))
             x = y
-    slot_b = max([hi - lo for _, lo, hi in parts], default=1)
-    s_h2d, s_cmp, s_d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-    dslot = [torch.empty(slot_b, dtype=torch.uint8, device=dev) for _ in range(2)]
-    hslot = [torch.empty(max(out_cap, 1), dtype=torch.uint8).pin_memory() for _ in range(2)]
-    ev_in = [torch.cuda.Event(), torch.cuda.Event()]      # piece landed in slot
-    ev_used = [torch.cuda.Event(), torch.cuda.Event()]    # replay done with slot
-    ev_out = [torch.cuda.Event(), torch.cuda.Event()]     # D2H done with host slot
+    host_parts = [chunks[k]["pinned"][lo:hi] for _, k, lo, hi in parts]
+    want_n = [int(np.searchsorted(chunks[k]["rec_off"].astype(np.int64), hi)
+                  - np.searchsorted(chunks[k]["rec_off"].astype(np.int64), lo)) for _, k, lo, hi in parts]
 
-    def h2d(i):
-        k, lo, hi = parts[i]
-        dslot[i & 1][: hi - lo].copy_(chunks[k]["pinned"][lo:hi], non_blocking=True)
-        ev_in[i & 1].record(s_h2d)
+    def check_part(i, hp):
+        assert hp.n == want_n[i] and not hp.end_error, ("part", i, hp.n, want_n[i], hp.end_error)
 
+    # checking pass (untimed): every value as it lands in host memory, CRC'd on the host (zlib),
+    # the keyed XOR over the rank's share equal to the device-only digest
+    t = time.perf_counter()
+    hd = [0]
+
+    def sink(i, hp):
+        check_part(i, hp)
+        f, _, lo, _ = parts[i]
+        hd[0] ^= replay.host_value_digest(hp, host_parts[i], lo, f)
+
+    part_cap = max([hi - lo for _, _, lo, hi in parts], default=1)
+    pipe_v = replay.ReplayPipeline(part_cap, "values", dev, ws, values_cap=out_cap)
+    pipe_v.run(host_parts, sink=sink)
+    assert hd[0] == digest_mine, f"end-to-end values: host digest {hd[0]:08x} != device-only {digest_mine:08x}"
+    log(f"rank {rank}: end-to-end values checked on the host ({len(parts)} parts, {time.perf_counter() - t:.1f}s)")
+
+    # the timed pass: the same pipeline with no host wait; the parts still in the two host slots
+    # at its end are checked against device-only replays of the same parts
     sync_all()
     t = time.perf_counter()
-    if parts:
-        with torch.cuda.stream(s_h2d):
-            h2d(0)
-    for i, (k, lo, hi) in enumerate(parts):
-        j = i & 1
-        if i + 1 < len(parts):   # prefetch the next piece while this one replays
-            with torch.cuda.stream(s_h2d):
-                if i >= 1:
-                    s_h2d.wait_event(ev_used[j ^ 1])
-                h2d(i + 1)
-        with torch.cuda.stream(s_cmp):
-            s_cmp.wait_event(ev_in[j])
-            r = replay.replay(dslot[j][: hi - lo], workspace=ws, stream=s_cmp)
-            ev_used[j].record(s_cmp)
-        with torch.cuda.stream(s_d2h):
-            s_d2h.wait_event(ev_used[j])
-            if i >= 2:
-                s_d2h.wait_event(ev_out[j])
-            nb = r.values.data.numel()
-            hslot[j][:nb].copy_(r.values.data, non_blocking=True)
-            r.values.data.record_stream(s_d2h)
-            ev_out[j].record(s_d2h)
+    got = pipe_v.run(host_parts)
     sync_all()
     pipe_s = time.perf_counter() - t
+    tail_checked = 0
+    for i, hp in enumerate(got):
+        if hp is None:
+            continue
+        check_part(i, hp)
+        f, k, lo, hi = parts[i]
+        res = replay.replay(chunks[k]["dev"][lo:hi], workspace=ws)
+        assert replay.host_value_digest(hp, host_parts[i], lo, f) == _value_digest(res, lo, f), ("timed part", i)
+        tail_checked += 1
+        del res
+    del got
 
     # ---- end to end as buildHintFromData needs it (store/bucket.go:89-117): the decompressed
     # body only feeds Getvhash and is freed (p.Free()), so per record only the hint fields travel
-    # back -- offset, the stored header (ver, ksz, vsz: the record size) and vhash ----
-    hmax = max([int(np.searchsorted(chunks[k]["rec_off"].astype(np.int64), hi)
-                    - np.searchsorted(chunks[k]["rec_off"].astype(np.int64), lo)) for k, lo, hi in parts], default=1)
-    hint_host = [dict(off=torch.empty(max(hmax, 1), dtype=torch.int64).pin_memory(),
-                      hdr=torch.empty((max(hmax, 1), 6), dtype=torch.int32).pin_memory(),
-                      vh=torch.empty(max(hmax, 1), dtype=torch.int32).pin_memory()) for _ in range(2)]
+    # back -- offset, the stored header (ver, ksz, vsz: the record size) and vhash.  Every part's
+    # hints stay in host memory: the timed pass itself is checked ----
+    pipe_h = replay.ReplayPipeline(part_cap, "hints", dev, ws, nparts=len(parts))
     sync_all()
     t = time.perf_counter()
-    if parts:
-        with torch.cuda.stream(s_h2d):
-            h2d(0)
-    for i, (k, lo, hi) in enumerate(parts):
-        j = i & 1
-        if i + 1 < len(parts):
-            with torch.cuda.stream(s_h2d):
-                if i >= 1:
-                    s_h2d.wait_event(ev_used[j ^ 1])
-                h2d(i + 1)
-        with torch.cuda.stream(s_cmp):
-            s_cmp.wait_event(ev_in[j])
-            r = replay.replay(dslot[j][: hi - lo], workspace=ws, stream=s_cmp)
-            ev_used[j].record(s_cmp)
-        with torch.cuda.stream(s_d2h):
-            s_d2h.wait_event(ev_used[j])
-            if i >= 2:
-                s_d2h.wait_event(ev_out[j])
-            hh, n = hint_host[j], r.n
-            hh["off"][:n].copy_(r.offset, non_blocking=True)
-            hh["hdr"][:n].copy_(r.header, non_blocking=True)
-            hh["vh"][:n].copy_(r.vhash, non_blocking=True)
-            for tsr in (r.offset, r.header, r.vhash):
-                tsr.record_stream(s_d2h)
-            ev_out[j].record(s_d2h)
+    hints = pipe_h.run(host_parts)
     sync_all()
     hint_s = time.perf_counter() - t
+    hh = 0
+    for i, hp in enumerate(hints):
+        check_part(i, hp)
+        f, _, lo, _ = parts[i]
+        hh ^= replay.hint_digest(hp.offset, hp.header, hp.vhash, lo, f)
+    assert hh == hdigest, f"end-to-end hints: host digest {hh:08x} != device-only {hdigest:08x}"
+    del hints, pipe_v, pipe_h
+    e2e_values = shard.xor_digest_over_ranks(hd[0], device=dev)
+    e2e_hints = shard.xor_digest_over_ranks(hh, device=dev)
+    hdigest = shard.xor_digest_over_ranks(hdigest, device=dev)
     dev_wall, dev_ev, pipe_s, hint_s = shard.max_over_ranks([dev_wall, dev_ev, pipe_s, hint_s], device=dev)
-    tot = shard.sum_over_ranks({"chunk": share, "out": out_mine, "records": nrec_mine, "pieces": len(pieces)},
+    tot = shard.sum_over_ranks({"chunk": share, "out": out_mine, "records": nrec_mine, "pieces": len(pieces),
+                                "parts": len(parts), "tail_checked": tail_checked},
                                device=dev)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -406,12 +403,24 @@ def run(a, rank: int, world: int, dev):
         "end_to_end_pipelined": {"total_gib": round(tot["chunk"] / 2**30, 2),
                                  "gib_per_s_chunk": round(tot["chunk"] / pipe_s / 2**30, 2),
                                  "seconds": round(pipe_s, 2),
-                                 "parts": len(parts), "part_mib": getattr(a, "pipe_mib", 4096),
-                                 "note": "each rank's pieces in parts cut at record starts: pinned H2D of part i+1, "
-                                         "replay of part i and pinned D2H of part i-1's decompressed values on three "
-                                         "streams"},
+                                 "parts": tot["parts"], "part_mib": getattr(a, "pipe_mib", 4096),
+                                 "digest": {"xor_value_crc32": f"{e2e_values:08x}",
+                                            "equals_device_only": e2e_values == digest,
+                                            "timed_parts_checked": tot["tail_checked"],
+                                            "what": "an untimed pass of the same pipeline CRCs every value on the host "
+                                                    "(zlib) as it lands in pinned memory, keyed like the device-only "
+                                                    "digest; the timed pass's last two parts (still in the host slots) "
+                                                    "are checked against device-only replays of the same parts; every "
+                                                    "part's record count and end state are asserted"},
+                                 "note": "replay.replay_pipelined: each rank's pieces in parts cut at record starts; "
+                                         "pinned H2D of part i+1, replay of part i and pinned D2H of part i-1's "
+                                         "decompressed values and per-record fields on three streams"},
         "end_to_end_hints": {"gib_per_s_chunk": round(tot["chunk"] / hint_s / 2**30, 2),
                              "seconds": round(hint_s, 2),
+                             "digest": {"xor_hint": f"{e2e_hints:08x}", "equals_device_only": e2e_hints == hdigest,
+                                        "what": "XOR over every record of a keyed mix of (offset, stored header, vhash) "
+                                                "as the timed pass left them in host memory, against the device-only "
+                                                "replay's"},
                              "note": "as buildHintFromData (store/bucket.go:89-117): the same pipeline, but the "
                                      "decompressed bodies stay on the device (they only feed Getvhash, p.Free()); "
                                      "per record offset, stored header and vhash go back (pinned D2H)"},
