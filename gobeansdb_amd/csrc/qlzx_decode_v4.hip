@@ -225,6 +225,9 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const ui
 #endif  // QLZX_K2_ONLY
 
 // ------------------------------------------------------------------------------- K2 ----
+#ifndef QLZX_K2_REL  // chunk phase on sources relative to the chunk (round 6)
+#define QLZX_K2_REL 1
+#endif
 constexpr uint32_t kV4W = 4096;   // output window (LDS ring)
 constexpr uint32_t kV4MR = 256;   // marker ring (u32 keys)
 constexpr uint32_t kV4Bpl = 4;  // output bytes per lane per chunk
@@ -384,7 +387,11 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
             constexpr uint32_t B = kV4Bpl;
             const uint32_t r0 = B * lane, p0 = c + r0;
             uint32_t *mkl = L.mk + ((c & (MR - 1)) + r0);
+#if QLZX_K2_REL
+            uint32_t m[B];
+#else
             uint32_t m[B], sv[B];
+#endif
 #pragma unroll
             for (uint32_t h = 0; h < B; h += 4) {
                 const uint4 q = *(const uint4 *)(mkl + h);
@@ -396,6 +403,61 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
             const uint32_t incl = v4_incl_max(lmax);
             uint32_t f = max(wave_shr1(incl), cin);
             cin = max(cin, (uint32_t)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(incl, 63)));
+#if QLZX_K2_REL
+            // sources relative to the chunk (rj = s - c mod 2^32): in-chunk sources of match bytes
+            // are s in [c, p), i.e. rj < r0 + j unsigned (a literal has rj = r0 + j, a source
+            // below c wraps above every in-chunk value), and the pointer jumping below compares
+            // and indexes the chunk's slots with rj directly
+            uint32_t rj[B];
+            bool qa[B], anyq = false;
+#pragma unroll
+            for (uint32_t j = 0; j < B; j++) {
+                f = max(f, m[j]);
+                rj[j] = r0 + j - (f & 0xffffu);
+                qa[j] = rj[j] < r0 + j;
+                anyq = anyq || qa[j];
+            }
+            PROF_MARK(1);
+            if (__ballot(anyq)) {
+                // the chunk's marker slots are free once read: they hold each byte's current source
+                uint32_t *spb = L.mk + (c & (MR - 1));
+#pragma unroll
+                for (uint32_t h = 0; h < B; h += 4) *(uint4 *)(mkl + h) = make_uint4(rj[h], rj[h + 1], rj[h + 2], rj[h + 3]);
+                do {
+                    uint32_t t[B];
+#pragma unroll
+                    for (uint32_t j = 0; j < B; j++) t[j] = spb[qa[j] ? rj[j] : r0 + j];
+                    uint64_t anym = 0;
+#pragma unroll
+                    for (uint32_t j = 0; j < B; j++) {
+                        // a byte whose source's source is outside the chunk or a literal is final
+                        qa[j] = t[j] < rj[j];
+                        anym |= __ballot(qa[j]);
+                        rj[j] = t[j];
+                    }
+                    anyq = anym != 0;
+#pragma unroll
+                    for (uint32_t h = 0; h < B; h += 4)
+                        *(uint4 *)(mkl + h) = make_uint4(rj[h], rj[h + 1], rj[h + 2], rj[h + 3]);
+                    PROF_COUNT(7, 1);
+                } while (anyq);
+            }
+            PROF_MARK(2);
+            // far: s < lo  <=>  rj < lo - c as signed (lo - c = MR - W once the window is full,
+            // else -c: nothing is below the block start)
+            const int32_t lo_rel = c + MR > W ? (int32_t)MR - (int32_t)W : -(int32_t)c;
+            uint32_t vb[B], sv[B];
+#pragma unroll
+            for (uint32_t j = 0; j < B; j++) {
+                sv[j] = rj[j] + c;
+                vb[j] = L.win[sv[j] & (W - 1)];
+            }
+            int32_t mn = (int32_t)rj[0];
+#pragma unroll
+            for (uint32_t j = 1; j < B; j++) mn = min(mn, (int32_t)rj[j]);
+            const bool far = mn < lo_rel;
+            const uint32_t lo = c + lo_rel;
+#else
             bool qa[B], anyq = false;
 #pragma unroll
             for (uint32_t j = 0; j < B; j++) {
@@ -441,6 +503,7 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
                 vb[j] = L.win[sv[j] & (W - 1)];
                 far = far || sv[j] < lo;
             }
+#endif
             PROF_COUNT(6, __ballot(far) ? 1 : 0);  // chunks with a byte older than the window
             uint32_t w[B / 4];
             if (__ballot(far)) {
