@@ -38,15 +38,13 @@ namespace qlzx {
 // c2 25.1-25.3 -> 24.7-24.9 ms at kmax 16; c4 346 -> 377 GiB/s at kmax 10
 // (tools/gpu_r5lr3.sh, profiles/r05_k1_lane_ring_ab.txt).
 #if (!defined(QLZX_K2_ONLY) && !QLZX_SPLIT_K1) || (defined(QLZX_K2_ONLY) && QLZX_SPLIT_K1)
-__global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
-                                                     int32_t *status, uint32_t first, uint32_t count, BlkInfo *info,
-                                                     GroupRec *recs, uint32_t gmax, const uint32_t *order,
-                                                     uint32_t max_dsize, uint32_t kmax) {
+// One wave's 64 blocks (lin = the block's place in the chunk), called by the kernel below.
+__device__ __forceinline__ void k1_parse_wave(uint8_t *ring, uint32_t lane, uint32_t lin, const qlzx_blocks &b,
+                                              const uint32_t *dst_cap, uint32_t *dsize_out, int32_t *status,
+                                              uint32_t first, uint32_t count, BlkInfo *info, GroupRec *recs,
+                                              uint32_t gmax, const uint32_t *order, uint32_t max_dsize,
+                                              uint32_t kmax) {
     constexpr uint32_t S = kRingSlots;
-    __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG / 64) * kRingWaveS<S>];
-    const uint32_t lane = threadIdx.x & 63;
-    uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWaveS<S>;
-    const uint32_t lin = blockIdx.x * kParseWG + threadIdx.x;
     const bool inrange = lin < count;
     const uint32_t i = inrange ? (order ? order[lin] : first + lin) : first;
 
@@ -120,59 +118,105 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const ui
         if (M >= 3 && (n) >= 3) *(u4v *)sl2 = v4, *(u4v *)(sl2 + 1024) = v5;                      \
         rl += (n);                                                                                \
     } while (0)
-    auto steps = [&]() __attribute__((always_inline)) {
-        const uint32_t lim = rl * kRoundBytes - shift;  // stream bytes below lim are in the ring
-        bool go = !done_parse;
-        uint32_t k = 0;
-        while (go) {  // per-lane loop, at most kmax steps
-            const bool gb = cwr == 1;
-            const uint32_t rem = csize - ip;
-            uint32_t run = __builtin_ctz(cwr);
-            run = run < rem ? run : rem;
-            const uint32_t q = ip + run;
-            const uint32_t rest = cwr >> run;
-            const bool hasm = !gb & (rest != 1u) & ((rest & 1u) != 0) & (q < csize);
-            const bool end = ip + (gb ? 4u : 1u) > csize;
-            const uint32_t need = gb ? 4u : 1u;
-            const bool landed = q + need <= lim;
-            const bool stepping = !end & ((gb | hasm) ? landed : true);
-            const uint32_t w = ring_rd32<S>(ring, q + shift, lane);
-            const uint32_t ty = (w & 3u) + ((w & 127u) == 3u ? 1u : 0u);
-            const uint32_t e = __builtin_amdgcn_ubfe(0x32110u, ty * 4, 4);
-            const uint32_t q2 = q + e + 1, rest2 = rest >> 1;
-            const bool hasm2 = hasm & (e < 3u) & ((rest2 & 1u) != 0) & (rest2 != 1u) & (q2 < csize) & (q2 + 1 <= lim);
-            const uint32_t w2 = w >> (8 * ((e + 1) & 3u));
-            const uint32_t ty2 = (w2 & 3u) + ((w2 & 127u) == 3u ? 1u : 0u);
-            const uint32_t e2 = hasm2 ? __builtin_amdgcn_ubfe(0x32110u, ty2 * 4, 4) : 0u;
-            const bool bad = stepping & ((gb & (((w >> 31) == 0) | (g >= gmax))) | (hasm & (q2 > csize)) |
-                                         (hasm2 & (q2 + e2 + 1 > csize)));
-            // the record store is invisible to the compiler's vmcnt bookkeeping: counted, it made
-            // every wait before the step loop a vmcnt(0), i.e. a wait for the loads just issued
-            // (an unseen store only makes the compiler's later vmcnt(N) waits stricter)
-            if (stepping & gb & (g > 0)) {
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 rec = {rec_ip, cwg, ra, rb};
-                asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(myrec + (g - 1)), "v"(rec) : "memory");
-            }
-            st = bad ? QLZX_E_CORRUPT : st;
-            const bool adv = stepping & !bad;
-            const uint32_t kb = hasm ? 1u << (__builtin_clz(cwr) + run) : 0u;
-            const uint32_t kb2 = hasm2 ? kb << 1 : 0u;
-            const uint32_t nip = gb ? ip + 4 : q + (hasm ? e + 1 : 0u) + (hasm2 ? e2 + 1 : 0u);
-            const uint32_t ncwr = gb ? w : (rest >> (hasm ? (hasm2 ? 2 : 1) : 0));
-            const uint32_t nra = gb ? 0u : (ra | ((e & 1u) ? kb : 0u) | ((e2 & 1u) ? kb2 : 0u));
-            const uint32_t nrb = gb ? 0u : (rb | ((e & 2u) ? kb : 0u) | ((e2 & 2u) ? kb2 : 0u));
-            rec_ip = (adv & gb) ? ip : rec_ip;
-            cwg = (adv & gb) ? w : cwg;
-            g += (adv & gb) ? 1u : 0u;
-            ip = adv ? nip : ip;
-            cwr = adv ? ncwr : cwr;
-            ra = adv ? nra : ra;
-            rb = adv ? nrb : rb;
-            done_parse = done_parse | end | bad;
-            go = adv && ++k < kmax;
-        }
+    // One step: a control word, or a literal run (ctz of the remaining control bits, no bytes
+    // read), the match that ends it and, when the next item is a match whose first byte is in the
+    // same dword, that one too.  Round 6 form (87 instead of 103 vector instructions per step,
+    // same checks in the same order as round 5's select-based step, in git history): a lane that
+    // cannot advance leaves the loop before anything is updated, the control-word and match cases
+    // update through a branch each, and the second token's byte is taken with one alignbyte.
+    // c2 time unchanged (23.77 vs 23.79 ms): K1's instructions cost c2 about half their issue
+    // time (+32 per step: +0.42 ms), DESIGN.md §3.
+    const uint32_t lane16 = lane << 4;
+    auto rd32 = [&](uint32_t x) __attribute__((always_inline)) -> uint32_t {  // ring_rd32<S>(ring, x, lane)
+        static_assert(S * kPieces == 8, "ring address below assumes 8 pieces of 1 KiB");
+        const uint32_t x4 = x + 4;
+        const uint32_t a1 = (__builtin_amdgcn_ubfe(x, 4, 3) << 10) | ((x & 12u) | lane16);
+        const uint32_t a2 = (__builtin_amdgcn_ubfe(x4, 4, 3) << 10) | ((x4 & 12u) | lane16);
+        const uint32_t lo = *(const uint32_t *)(ring + a1);
+        const uint32_t hi = *(const uint32_t *)(ring + a2);
+        return __builtin_amdgcn_alignbyte(hi, lo, x);
     };
+    // token bytes - 1 from the token's first byte (quicklz.c:579-610): 0, 1, 1, 2 by b & 3,
+    // 3 when b & 127 == 3
+    auto tlc = [](uint32_t b) __attribute__((always_inline)) -> uint32_t {
+        return __builtin_amdgcn_ubfe(0x94u, (b & 3u) * 2, 2) + ((b & 127u) == 3u ? 1u : 0u);
+    };
+    auto steps = [&]() __attribute__((always_inline)) -> uint32_t {
+        const uint32_t lim = rl * kRoundBytes - shift;  // stream bytes below lim are in the ring
+        uint32_t k = 0;
+        if (!done_parse) {
+            for (;;) {  // per-lane loop, at most kmax steps
+                const bool gb = cwr == 1;
+                const uint32_t run = min((uint32_t)__builtin_ctz(cwr), csize - ip);
+                const uint32_t q = ip + run;
+                const uint32_t rest = cwr >> run;
+                // a match at q (gb: rest == 1; a run cut by the stream end: q == csize)
+                const bool hasm = (rest > 1u) & (q < csize);
+                const uint32_t need = gb ? 4u : 1u;
+                if (ip + need > csize) {  // the stream ends here (C1/C5 are K2's or the caller's)
+                    done_parse = true;
+                    break;
+                }
+                if ((gb | hasm) & (q + need > lim)) break;  // wait for the ring
+                const uint32_t w = rd32(q + shift);
+                const uint32_t e = tlc(w);
+                const uint32_t q2 = q + e + 1, rest2 = rest >> 1;
+                const bool hasm2 = hasm & (e < 3u) & ((rest2 & 1u) != 0) & (rest2 > 1u) & (q2 < csize) & (q2 < lim);
+                const uint32_t e2 = hasm2 ? tlc(__builtin_amdgcn_alignbyte(0u, w, e + 1)) : 0u;
+                const bool bad = (gb & (((int32_t)w >= 0) | (g >= gmax))) | (hasm & (q2 > csize)) |
+                                 (hasm2 & (q2 + e2 + 1 > csize));
+                if (bad) {
+                    st = QLZX_E_CORRUPT;
+                    done_parse = true;
+                    break;
+                }
+                if (gb) {
+                    // the record store is invisible to the compiler's vmcnt bookkeeping: counted, it
+                    // made every wait before the step loop a vmcnt(0), i.e. a wait for the loads just
+                    // issued (an unseen store only makes the compiler's later vmcnt(N) waits stricter)
+                    if (g > 0) {
+                        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                        const u32x4 rec = {rec_ip, cwg, ra, rb};
+                        asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(myrec + (g - 1)), "v"(rec) : "memory");
+                    }
+                    rec_ip = ip;
+                    cwg = w;
+                    g++;
+                    ip += 4;
+                    cwr = w;
+                    ra = 0;
+                    rb = 0;
+                } else {
+                    const uint32_t idx = __builtin_clz(cwr) + run;  // item index of the match
+                    const uint32_t em = hasm ? e : 0u, e2m = hasm2 ? e2 : 0u;
+                    ra |= ((em & 1u) | ((e2m & 1u) << 1)) << idx;
+                    rb |= ((em >> 1) | (e2m & 2u)) << idx;
+                    ip = q + em + e2m + (hasm ? 1u : 0u) + (hasm2 ? 1u : 0u);
+                    cwr = rest >> ((hasm ? 1u : 0u) + (hasm2 ? 1u : 0u));
+                }
+                if (++k >= kmax) break;
+            }
+        }
+        return k;
+    };
+#ifdef QLZX_PROFILE
+    // profile build: outer iterations, wave step trips (max steps over lanes per iteration) and
+    // lane steps (sum over lanes) per wave, in slot 0
+    PROF_DECL
+    auto k1prof = [&](uint32_t k) __attribute__((always_inline)) {
+        uint32_t mx = k, sm = k;
+        for (int o = 32; o >= 1; o >>= 1) {
+            mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+            sm += (uint32_t)__shfl_xor((int)sm, o);
+        }
+        PROF_COUNT(0, 1);
+        PROF_COUNT(1, mx);
+        PROF_COUNT(2, sm);
+    };
+#define K1_STEPS() k1prof(steps())
+#else
+#define K1_STEPS() (void)steps()
+#endif
 
     u4v pa0, pa1, pa2, pa3, pa4, pa5, pb0, pb1, pb2, pb3, pb4, pb5;
     uint32_t na = accept();
@@ -191,21 +235,27 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const ui
         K1_STORE(na, pa0, pa1, pa2, pa3, pa4, pa5);
         nb = accept();
         K1_LOAD(nb, pb0, pb1, pb2, pb3, pb4, pb5);
-        steps();
+        K1_STEPS();
         guard();
         if (__ballot(!done_parse) == 0) break;
         K1_STORE(nb, pb0, pb1, pb2, pb3, pb4, pb5);
         na = accept();
         K1_LOAD(na, pa0, pa1, pa2, pa3, pa4, pa5);
-        steps();
+        K1_STEPS();
         guard();
         if (__ballot(!done_parse) == 0) break;
     }
 #undef K1_LD
 #undef K1_LOAD
 #undef K1_STORE
+#undef K1_STEPS
     if (parsing && st == QLZX_OK && g > 0) myrec[g - 1] = GroupRec{rec_ip, cwg, ra, rb};
     vm_sync();
+#ifdef QLZX_PROFILE
+    PROF_MARK(3);
+    PROF_COUNT(4, 1);
+    PROF_FLUSH(0);
+#endif
     if (!inrange) return;
     if (st == QLZX_OK && kind == kBlkCompressed && (!done_parse || g == 0)) st = QLZX_E_CORRUPT;
     BlkInfo bi{0, 0, kind, dsize};
@@ -222,12 +272,21 @@ __global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const ui
     }
     info[lin] = bi;
 }
+
+__global__ void __launch_bounds__(kParseWG) k_dec_parse6(qlzx_blocks b, const uint32_t *dst_cap, uint32_t *dsize_out,
+                                                     int32_t *status, uint32_t first, uint32_t count, BlkInfo *info,
+                                                     GroupRec *recs, uint32_t gmax, const uint32_t *order,
+                                                     uint32_t max_dsize, uint32_t kmax) {
+    constexpr uint32_t S = kRingSlots;
+    __shared__ __attribute__((aligned(16))) uint8_t ring_all[(kParseWG / 64) * kRingWaveS<S>];
+    const uint32_t lane = threadIdx.x & 63;
+    uint8_t *ring = ring_all + (threadIdx.x >> 6) * kRingWaveS<S>;
+    k1_parse_wave(ring, lane, blockIdx.x * kParseWG + threadIdx.x, b, dst_cap, dsize_out, status, first, count, info,
+                  recs, gmax, order, max_dsize, kmax);
+}
 #endif  // QLZX_K2_ONLY
 
 // ------------------------------------------------------------------------------- K2 ----
-#ifndef QLZX_K2_REL  // chunk phase on sources relative to the chunk (round 6)
-#define QLZX_K2_REL 1
-#endif
 constexpr uint32_t kV4W = 4096;   // output window (LDS ring)
 constexpr uint32_t kV4MR = 256;   // marker ring (u32 keys)
 constexpr uint32_t kV4Bpl = 4;  // output bytes per lane per chunk
@@ -303,7 +362,7 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
     PROF_DECL
     uint32_t D = 0, bt = 0, c = 0, cin = 0;
     bool tail = false, complete = false, err = false;
-    uint64_t pend = 0;
+    bool pend = false, mp = false;  // some lane's item / this lane's item waits for its marker slot
     uint32_t pd = 0, pkey = 0;
     uint32_t plit = 0;
 
@@ -312,12 +371,12 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
     auto batch = [&](uint32_t posm, uint32_t tok, const GroupRec &gr_next, uint32_t &posm_n, uint32_t &tok_n,
                      GroupRec &gr_nn) __attribute__((always_inline)) {
         if (pend) {  // a straddling batch's items not marked by a chunk yet (all start below c + CH)
-            const bool wr = (pend >> lane) & 1u;
+            const bool wr = mp;
             if (wr) {
                 L.mk[pd & (MR - 1)] = pkey;
                 if (plit < 0x100u) L.win[pd & (W - 1)] = (uint8_t)plit;
             }
-            pend = 0;
+            pend = mp = false;
         }
         const bool v = bt * 64 + lane < nitems;
         {
@@ -364,7 +423,8 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
             // gather reads before the chunk of d overwrites it: the byte can go there unconditionally
             L.win[d & (W - 1)] = (uint8_t)t;
         }
-        pend = __ballot(live && !wr);
+        mp = live && !wr;
+        pend = __ballot(mp) != 0;
         pd = d;
         pkey = key;
         plit = ism ? 0x100u : (t & 0xffu);
@@ -377,21 +437,18 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
     auto chunks = [&]() __attribute__((always_inline)) -> bool {
         while (c < dsize && (complete || D >= c + CH)) {
             if (pend) {  // items of the last batch that start at or above c_prev + MR
-                const bool wr = ((pend >> lane) & 1u) && pd < c + MR;
+                const bool wr = mp && pd < c + MR;
                 if (wr) {
                     L.mk[pd & (MR - 1)] = pkey;
                     if (plit < 0x100u) L.win[pd & (W - 1)] = (uint8_t)plit;
                 }
-                pend &= ~__ballot(wr);
+                mp = mp && !wr;
+                pend = __ballot(mp) != 0;
             }
             constexpr uint32_t B = kV4Bpl;
             const uint32_t r0 = B * lane, p0 = c + r0;
             uint32_t *mkl = L.mk + ((c & (MR - 1)) + r0);
-#if QLZX_K2_REL
             uint32_t m[B];
-#else
-            uint32_t m[B], sv[B];
-#endif
 #pragma unroll
             for (uint32_t h = 0; h < B; h += 4) {
                 const uint4 q = *(const uint4 *)(mkl + h);
@@ -403,7 +460,6 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
             const uint32_t incl = v4_incl_max(lmax);
             uint32_t f = max(wave_shr1(incl), cin);
             cin = max(cin, (uint32_t)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(incl, 63)));
-#if QLZX_K2_REL
             // sources relative to the chunk (rj = s - c mod 2^32): in-chunk sources of match bytes
             // are s in [c, p), i.e. rj < r0 + j unsigned (a literal has rj = r0 + j, a source
             // below c wraps above every in-chunk value), and the pointer jumping below compares
@@ -441,6 +497,7 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
                         *(uint4 *)(mkl + h) = make_uint4(rj[h], rj[h + 1], rj[h + 2], rj[h + 3]);
                     PROF_COUNT(7, 1);
                 } while (anyq);
+
             }
             PROF_MARK(2);
             // far: s < lo  <=>  rj < lo - c as signed (lo - c = MR - W once the window is full,
@@ -457,53 +514,6 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
             for (uint32_t j = 1; j < B; j++) mn = min(mn, (int32_t)rj[j]);
             const bool far = mn < lo_rel;
             const uint32_t lo = c + lo_rel;
-#else
-            bool qa[B], anyq = false;
-#pragma unroll
-            for (uint32_t j = 0; j < B; j++) {
-                f = max(f, m[j]);
-                sv[j] = p0 + j - (f & 0xffffu);
-                // in-chunk sources of match bytes: s in [c, p)  <=>  s - c < p - c (unsigned)
-                qa[j] = sv[j] - c < r0 + j;
-                anyq = anyq || qa[j];
-            }
-            PROF_MARK(1);
-            const uint32_t lo = c + MR > W ? c + MR - W : 0u;
-            if (__ballot(anyq)) {
-                // the chunk's marker slots are free once read: they hold each byte's current source
-                uint32_t *spb = L.mk + (c & (MR - 1));
-#pragma unroll
-                for (uint32_t h = 0; h < B; h += 4) *(uint4 *)(mkl + h) = make_uint4(sv[h], sv[h + 1], sv[h + 2], sv[h + 3]);
-                do {
-                    uint32_t t[B];
-#pragma unroll
-                    for (uint32_t j = 0; j < B; j++) t[j] = spb[(qa[j] ? sv[j] : p0 + j) - c];
-                    // the wave's "any byte still jumping" as an OR of per-byte ballots (scalar
-                    // masks), not an OR of the lanes' bools (packed into a bit vector per lane)
-                    uint64_t anym = 0;
-#pragma unroll
-                    for (uint32_t j = 0; j < B; j++) {
-                        // a byte whose source's source is outside the chunk or a literal is final
-                        qa[j] = t[j] - c < sv[j] - c;
-                        anym |= __ballot(qa[j]);
-                        sv[j] = t[j];
-                    }
-                    anyq = anym != 0;
-#pragma unroll
-                    for (uint32_t h = 0; h < B; h += 4)
-                        *(uint4 *)(mkl + h) = make_uint4(sv[h], sv[h + 1], sv[h + 2], sv[h + 3]);
-                    PROF_COUNT(7, 1);
-                } while (anyq);
-            }
-            PROF_MARK(2);
-            uint32_t vb[B];
-            bool far = false;
-#pragma unroll
-            for (uint32_t j = 0; j < B; j++) {
-                vb[j] = L.win[sv[j] & (W - 1)];
-                far = far || sv[j] < lo;
-            }
-#endif
             PROF_COUNT(6, __ballot(far) ? 1 : 0);  // chunks with a byte older than the window
             uint32_t w[B / 4];
             if (__ballot(far)) {

@@ -282,6 +282,9 @@ int launch_k2_nocrc(uint32_t grid, hipStream_t s, const qlzx_blocks &b, uint32_t
                     uint32_t first, uint32_t cnt, const BlkInfo *info, const GroupRec *recs, uint32_t gmax,
                     const uint32_t *order);
 #endif
+// K1's grid: one wave per 64 blocks (persistent K1 waves, 512-2048 of them, made K1 the critical
+// path: c2 24.2-35.7 ms against 23.8, DESIGN.md history, round 6)
+inline uint32_t k1_grid(uint32_t cnt) { return (cnt + kParseWG - 1) / kParseWG; }
 inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uint32_t *dsize,
                               int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
                               uint32_t *crc_out, uint32_t max_dsize, void *ws, size_t ws_bytes,
@@ -385,11 +388,11 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         // QLZX_K1_KMAX_MIX (10) for mixed sizes (c4: 377 vs 363 GiB/s; c5 580 vs 560)
 #if QLZX_SPLIT_K1
         // the helpers return hipGetLastError(), which also clears the error: keep it here
-        if (const int e1 = launch_k1_parse6((cnt + kParseWG - 1) / kParseWG, s1, b, dst_cap, dsize, status, first, cnt, info, recs,
+        if (const int e1 = launch_k1_parse6(k1_grid(cnt), s1, b, dst_cap, dsize, status, first, cnt, info, recs,
                                gmax, order, max_dsize, max_dsize > 16384 ? (uint32_t)QLZX_K1_KMAX_MIX : (uint32_t)QLZX_K1_KMAX_UNI))
             return e1;
 #else
-        hipLaunchKernelGGL(k_dec_parse6, dim3((cnt + kParseWG - 1) / kParseWG), dim3(kParseWG), 0, s1, b, dst_cap, dsize,
+        hipLaunchKernelGGL(k_dec_parse6, dim3(k1_grid(cnt)), dim3(kParseWG), 0, s1, b, dst_cap, dsize,
                            status, first, cnt, info, recs, gmax, order, max_dsize, max_dsize > 16384 ? (uint32_t)QLZX_K1_KMAX_MIX : (uint32_t)QLZX_K1_KMAX_UNI);
 #endif
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], s1), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);

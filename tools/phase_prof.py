@@ -44,10 +44,11 @@ waves_k1 = (n + 63) // 64
 rounds = csum / n / 64
 batches = n * 3817 / 64
 print(f"blocks {n} x {bs} {kind}: wall {1e3 * (t1 - t0):.2f} ms, ratio {csum / (n * bs):.3f}")
-names1 = ["pre-loop", "wait DMA", "CRC", "parse", "issue+end"]
-print("K1 per wave per round (cycles):", {nm: round(p[j] / waves_k1 / rounds) for j, nm in enumerate(names1)})
-print("K1 parse iterations per wave-round: %.1f, active lanes per iteration (lane 0 only sampled): %.2f"
-      % (p[5] / waves_k1 / rounds, p[6] / max(p[5], 1)))
+# K1 k_dec_parse6 (slot 0): outer iterations, wave step trips, lane steps, cycles, waves
+k1 = p[0:8]
+w1 = max(k1[4], 1)
+print("K1 per wave: iterations %.1f, wave step trips %.1f, lane steps per lane %.1f (lane efficiency %.2f), "
+      "cycles %.0f" % (k1[0] / w1, k1[1] / w1, k1[2] / w1 / 64, k1[2] / max(64 * k1[1], 1), k1[3] / w1))
 # K2 = k_dec_bytes: stamps 0..4 are phases, 5..7 counts (slot 1 = p[8:16])
 names2 = ["item phase", "markers+fill", "pointer jumping", "gather", "store"]
 k2 = p[8:16]
