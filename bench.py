@@ -78,6 +78,8 @@ def parse():
                    help="c2 run: skip the c4 .data replay leg reported under \"replay\" in the same line")
     p.add_argument("--c4-chunk-mib", type=int, default=4000, help="c4 leg: MiB per chunk file (two distinct)")
     p.add_argument("--c4-files", type=int, default=13, help="c4 leg: files in the corpus (~50 GiB)")
+    p.add_argument("--no-record", action="store_true", help="c2 run: skip the f3 record-encode leg")
+    p.add_argument("--record-values", type=int, default=1 << 18, help="f3 leg: values per GPU (16 KiB text)")
     p.add_argument("--crc", action="store_true", help="fused record CRC verify in the timed pass")
     p.add_argument("--no-crc-leg", action="store_true",
                    help="skip the \"crc\" leg (the c2 shard again with the fused CRC verify)")
@@ -332,6 +334,13 @@ def main():
         replay_rec = c4mod.run(a4, rank, world, dev)
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+    enc_rec = None
+    if not args.no_record and legs:
+        # write-side record encode (TryCompress + encodeHeader + CRC + padding) of distinct
+        # 16 KiB text values, device-resident
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        enc_rec = bench_record_encode(args, rank, world, dev)
     mixed = None
     if not args.no_c5 and legs:
         # BASELINE config c5 in the same run: one 400 GiB corpus of distinct mixed 4-64 KiB values
@@ -349,6 +358,8 @@ def main():
                                                     "roofline", "cpu_baseline")}
         if replay_rec is not None:
             rec["replay"] = replay_rec
+        if enc_rec is not None:
+            rec["record_encode"] = enc_rec
         if mixed is not None:
             rec["mixed"] = {k: mixed[k] for k in ("metric", "value", "unit", "scaling", "rounds_per_gpu", "wall_s",
                                                   "incl_h2d", "digest", "config", "roofline")}
@@ -360,6 +371,58 @@ def main():
 
 
 SEED = 0x5EED2026
+
+
+def bench_record_encode(args, rank, world, dev):
+    """SURVEY f3 (store/item.go:114-161, store/datafile.go:66-88,307-330): record.encode of this
+    rank's distinct 16 KiB text values with keys "key_%016x" -- the TryCompress trial (10 KiB) and
+    full compress, the record CRC and the 256-B padded layout, all batched on the device.  Checked:
+    the records replay (qlzx_replay_index + decompress) to the original values (an XOR of value
+    CRCs).  Returns the leg's record on rank 0 (max-over-ranks time, summed bytes)."""
+    from gobeansdb_amd import batch, record, replay, shard
+    n = max(1, (args.record_values >> 4) if args.legs_small else args.record_values)
+    bs = 16384
+    first = rank * n
+    vals = batch.synth("text", SEED + 3, [bs] * n, first_id=first, device=dev)
+    keys = [b"key_%016x" % (first + i) for i in range(n)]
+    ws = batch.Workspace(dev)
+    enc = record.encode(keys, vals, workspace=ws)
+    torch.cuda.synchronize()
+    rr = replay.replay(enc.data, workspace=ws)
+    torch.cuda.synchronize()
+    assert rr.n == n and not rr.end_error and int(rr.size_broken.abs().sum()) == 0, (rr.n, n)
+    assert int(((rr.flag & 0x10000) != 0).sum()) == 0, "a stored value failed to decode"
+    want = shard.xor_of(batch.crc32(vals))
+    got = shard.xor_of(rr.value_crcs())
+    assert got == want, "record encode round trip: value digest differs"
+    rec_bytes = int(enc.data.numel())
+    ncomp = int((enc.flag & 0x10000 != 0).sum())
+    del rr, enc
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    steps = max(1, min(args.steps, 3))
+    t = time.perf_counter()
+    for _ in range(steps):
+        record.encode(keys, vals, workspace=ws)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    sec = shard.max_over_ranks([(time.perf_counter() - t) / steps], device=dev)[0]
+    tot = shard.sum_over_ranks({"values": n, "in": n * bs, "out": rec_bytes, "comp": ncomp}, device=dev)
+    if rank != 0:
+        return None
+    alg = tot["in"] + tot["out"]
+    return {"value": round(tot["in"] / sec / 2**30, 2), "unit": "GiB/s of values in",
+            "records_per_s": round(tot["values"] / sec), "ms_per_call": round(sec * 1e3, 2), "steps": steps,
+            "config": {"workload": f"f3: record.encode of {n} distinct {bs} B text values per GPU (keys key_%016x), "
+                                   f"device-resident; {tot['comp']} stored compressed", "values_per_gpu": n},
+            "digest_check": "the records replay to the original values (XOR of value crc32 equal)",
+            "roofline": {"bound": "hbm", "achieved": round(alg / sec / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(alg / sec / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                         "what": "algorithmic bytes: every value byte read once + every record byte written once; "
+                                 "the call also compresses a 10 KiB trial and the whole body (TryCompress) and "
+                                 "syncs the host between its steps (sizes, flags)"}}
 
 
 def bench_standin(args, rank, world):

@@ -293,8 +293,9 @@ constexpr uint32_t kV4Bpl = 4;  // output bytes per lane per chunk
 constexpr uint32_t kV4Chunk = 64 * kV4Bpl;      // 256 or 512 output bytes per chunk
 static_assert(kV4Chunk <= kV4MR, "a chunk's pointer-jumping array lives in its marker slots");
 
+template <uint32_t W = kV4W>
 struct K2v4Lds {
-    uint8_t win[kV4W];
+    uint8_t win[W];
     uint32_t mk[kV4MR];
 };
 
@@ -309,10 +310,11 @@ __device__ __forceinline__ uint32_t v4_incl_max(uint32_t v) {
     return v;
 }
 
-__device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uint8_t *dst, uint32_t csize,
+template <uint32_t WIN>
+__device__ __forceinline__ void dec_v4_block(K2v4Lds<WIN> &L, const uint8_t *src, uint8_t *dst, uint32_t csize,
                                              const BlkInfo bi, const GroupRec *rb, int32_t *status_i,
                                              uint32_t *dsize_i, uint32_t lane) {
-    constexpr uint32_t W = kV4W, MR = kV4MR, CH = kV4Chunk;
+    constexpr uint32_t W = WIN, MR = kV4MR, CH = kV4Chunk;
     const uint32_t dsize = bi.dsize;
     if (bi.kind == kBlkStored) {  // quicklz.c:808-811
         const uint32_t hdr = (src[0] & 2u) ? 9u : 3u;
@@ -557,18 +559,18 @@ __device__ __forceinline__ void dec_v4_block(K2v4Lds &L, const uint8_t *src, uin
     }
 }
 
-template <bool CRC>
+template <bool CRC, uint32_t WIN = kV4W>
 __global__ void __launch_bounds__(64) k_dec_chunk4(qlzx_blocks b, uint32_t *dsize_out, int32_t *status,
                                                    uint32_t first, uint32_t count, const BlkInfo *info,
                                                    const GroupRec *recs, uint32_t gmax, const uint32_t *list,
                                                    const uint32_t *crc_state, const uint32_t *crc_expect,
                                                    uint32_t *crc_out) {
-    __shared__ __attribute__((aligned(16))) K2v4Lds L;
+    __shared__ __attribute__((aligned(16))) K2v4Lds<WIN> L;
     const uint32_t bx = blockIdx.x;
     if (bx >= count) return;
     const uint32_t i = list ? list[bx] : first + bx;
     if constexpr (CRC) {
-        static_assert(sizeof(K2v4Lds) >= 4096, "the slicing-by-4 CRC tables fill 4 KiB of the window");
+        static_assert(sizeof(K2v4Lds<WIN>) >= 4096, "the slicing-by-4 CRC tables fill 4 KiB of the window");
         const uint32_t lane = threadIdx.x;
         uint32_t *tab = (uint32_t *)&L;
         for (uint32_t e = lane * 4; e < 1024; e += 256) *(uint4 *)(tab + e) = *(const uint4 *)(g_crc_slice8 + e);

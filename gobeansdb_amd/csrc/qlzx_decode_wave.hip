@@ -280,7 +280,7 @@ int launch_k1_parse6(uint32_t grid, hipStream_t s, const qlzx_blocks &b, const u
 #if QLZX_SPLIT_K2  // K2 without CRC lives in qlzx_k2.hip (its own scheduler strategy)
 int launch_k2_nocrc(uint32_t grid, hipStream_t s, const qlzx_blocks &b, uint32_t *dsize, int32_t *status,
                     uint32_t first, uint32_t cnt, const BlkInfo *info, const GroupRec *recs, uint32_t gmax,
-                    const uint32_t *order);
+                    const uint32_t *order, bool big);
 #endif
 // K1's grid: one wave per 64 blocks (persistent K1 waves, 512-2048 of them, made K1 the critical
 // path: c2 24.2-35.7 ms against 23.8, DESIGN.md history, round 6)
@@ -403,7 +403,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         else
 #if QLZX_SPLIT_K2
             if (const int e2 = launch_k2_nocrc(cnt, s, b, dsize, status, first, cnt, info, recs, gmax,
-                                               (const uint32_t *)order))
+                                               (const uint32_t *)order, max_dsize > 16384))
                 return e2;
 #else
             hipLaunchKernelGGL(k_dec_chunk4<false>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,

@@ -26,7 +26,13 @@ namespace qlzx {
 
 int launch_k2_nocrc(uint32_t grid, hipStream_t s, const qlzx_blocks &b, uint32_t *dsize, int32_t *status,
                     uint32_t first, uint32_t cnt, const BlkInfo *info, const GroupRec *recs, uint32_t gmax,
-                    const uint32_t *order) {
+                    const uint32_t *order, bool big) {
+#if QLZX_K2_BIGW  // an 8 KiB window for calls of values over 16 KiB (fewer far loads, fewer waves per SIMD)
+    if (big)
+        hipLaunchKernelGGL((k_dec_chunk4<false, 8192>), dim3(grid), dim3(64), 0, s, b, dsize, status, first, cnt, info,
+                           recs, gmax, order, nullptr, nullptr, nullptr);
+    else
+#endif
     hipLaunchKernelGGL(k_dec_chunk4<false>, dim3(grid), dim3(64), 0, s, b, dsize, status, first, cnt, info, recs,
                        gmax, order, nullptr, nullptr, nullptr);
     return (int)hipGetLastError();

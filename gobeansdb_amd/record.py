@@ -90,9 +90,28 @@ def _dev_u32(a, dev):
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(dev)
 
 
+def sniff_many(heads: np.ndarray, lens: np.ndarray, not_compress=NOT_COMPRESS) -> np.ndarray:
+    """need_compress for many values at once: heads = the first bytes of each value (uint8
+    [n, >= 12]), lens = the value lengths.  Same rows, order and masks as sniff()."""
+    n = len(lens)
+    undecided = np.ones(n, bool)
+    skip = np.zeros(n, bool)
+    for mask, pat, name in _AV_SIGS:   # the first matching row decides, as in sniff()
+        k = len(pat)
+        m = np.frombuffer(mask, np.uint8)[None, :]
+        hit = undecided & (lens >= k) & np.all((heads[:, :k] & m) == np.frombuffer(pat, np.uint8)[None, :], axis=1)
+        if name in not_compress:
+            skip |= hit
+        undecided &= ~hit
+    if None in not_compress:   # "some other answer" listed: every value without an audio/video row
+        skip |= undecided
+    return ~skip
+
+
 def encode(keys: list[bytes], values: batch.BlockBatch, flags=None, vers=None, ts=None,
            not_compress=NOT_COMPRESS, workspace: batch.Workspace | None = None, stream=None) -> Encoded:
-    """TryCompress + encodeHeader + padding for n records whose values live on the device."""
+    """TryCompress + encodeHeader + padding for n records whose values live on the device.
+    Every per-record step is a device batch or a numpy array operation (no per-record host loop)."""
     L = _lib.lib()
     dev = values.data.device
     n = values.n
@@ -102,18 +121,22 @@ def encode(keys: list[bytes], values: batch.BlockBatch, flags=None, vers=None, t
     ts = np.zeros(n, np.uint32) if ts is None else np.asarray(ts, np.uint32)
     vlen = values.length.cpu().numpy().view(np.uint32).astype(np.int64)
     voff = values.off.cpu().numpy().view(np.uint64)
-    klen = np.asarray([len(k) for k in keys], np.int64)
+    klen = np.fromiter(map(len, keys), np.int64, count=n)
 
     # ---- TryCompress candidates (store/item.go:121-137) ----
     padded = (HDR + klen + vlen + 255) // 256 * 256
     cand = (vers >= 0) & ((flags & (FLAG_CLIENT_COMPRESS | FLAG_COMPRESS)) == 0) & (padded > PADDING)
     ci = np.nonzero(cand)[0]
     if len(ci):
-        # sniff the first 512 bytes of each candidate (gathered from the device)
-        heads = _gather_prefix(values, ci, 512)
-        ok = np.asarray([need_compress(h, not_compress) for h in heads], bool)
+        # MIME sniff (item.go:114-118) on the first bytes of each candidate, gathered from the device
+        ok = sniff_many(_gather_heads(values, ci, 16), vlen[ci], not_compress)
         ci = ci[ok]
-    comp_body = {}   # record -> (device buffer, offset, length, raw value crc)
+    is_comp = np.zeros(n, bool)
+    c_src = np.zeros(n, np.int8)      # 0: the trial's output buffer, 1: the full compress's
+    c_off = np.zeros(n, np.uint64)
+    c_len = np.zeros(n, np.int64)
+    c_crc = np.zeros(n, np.uint32)    # raw CRC (state 0) of the compressed value
+    bufs = [None, None]
     if len(ci):
         tlen = np.minimum(vlen[ci], TRY_COMPRESS_SIZE)
         trial = batch.BlockBatch(values.data, _dev_u64(voff[ci], dev), _dev_u32(tlen, dev))
@@ -124,11 +147,14 @@ def encode(keys: list[bytes], values: batch.BlockBatch, flags=None, vers=None, t
         if int((tst != 0).sum()):
             raise _lib.QlzxError("trial compress failed on the device")
         keep = (tcs_h.astype(np.float32) / tlen.astype(np.float32)) <= COMPRESS_RATIO_LIMIT   # :145
-        tcrc_h = tcrc.cpu().numpy().view(np.uint32)
-        toff_h = tdst.off.cpu().numpy().view(np.uint64)
         full = keep & (vlen[ci] > tlen)      # :149-156: recompress the whole body
-        for j in np.nonzero(keep & ~full)[0]:
-            comp_body[int(ci[j])] = (tdst.data, int(toff_h[j]), int(tcs_h[j]), int(tcrc_h[j]) ^ 0xFFFFFFFF)
+        kt = keep & ~full
+        bufs[0] = tdst.data
+        r = ci[kt]
+        is_comp[r] = True
+        c_off[r] = tdst.off.cpu().numpy().view(np.uint64)[kt]
+        c_len[r] = tcs_h[kt]
+        c_crc[r] = tcrc.cpu().numpy().view(np.uint32)[kt] ^ np.uint32(0xFFFFFFFF)
         fi = ci[full]
         if len(fi):
             fsrc = batch.BlockBatch(values.data, _dev_u64(voff[fi], dev), _dev_u32(vlen[fi], dev))
@@ -137,43 +163,49 @@ def encode(keys: list[bytes], values: batch.BlockBatch, flags=None, vers=None, t
                                                  workspace=ws, stream=stream)
             if int((fst != 0).sum()):
                 raise _lib.QlzxError("compress failed on the device")
-            fcs_h = fcs.cpu().numpy().view(np.uint32).astype(np.int64)
-            fcrc_h = fcrc.cpu().numpy().view(np.uint32)
-            foff_h = fdst.off.cpu().numpy().view(np.uint64)
-            for j, r in enumerate(fi):
-                comp_body[int(r)] = (fdst.data, int(foff_h[j]), int(fcs_h[j]), int(fcrc_h[j]) ^ 0xFFFFFFFF)
+            bufs[1] = fdst.data
+            is_comp[fi] = True
+            c_src[fi] = 1
+            c_off[fi] = fdst.off.cpu().numpy().view(np.uint64)
+            c_len[fi] = fcs.cpu().numpy().view(np.uint32).astype(np.int64)
+            c_crc[fi] = fcrc.cpu().numpy().view(np.uint32) ^ np.uint32(0xFFFFFFFF)
     # ---- stored value sizes / flags ----
-    vsz = vlen.copy()
-    for r, (_, _, cl, _) in comp_body.items():
-        vsz[r] = cl
-        flags[r] += FLAG_COMPRESS                                   # :159
+    vsz = np.where(is_comp, c_len, vlen)
+    flags = flags + np.where(is_comp, np.uint32(FLAG_COMPRESS), np.uint32(0)).astype(np.uint32)   # :159
     # ---- raw CRC (from state 0) of every stored value ----
-    raw_v = np.zeros(n, np.uint32)
-    plain = np.asarray([r for r in range(n) if r not in comp_body], np.int64)
+    raw_v = c_crc.copy()
+    plain = np.nonzero(~is_comp)[0]
     if len(plain):
         c = batch.crc32(batch.BlockBatch(values.data, _dev_u64(voff[plain], dev), _dev_u32(vlen[plain], dev)),
                         init=torch.zeros(len(plain), dtype=torch.int32, device=dev), final_xor=0, stream=stream)
         raw_v[plain] = c.cpu().numpy().view(np.uint32)
-    for r, (_, _, _, rc) in comp_body.items():
-        raw_v[r] = rc
-    # ---- header[4:24] ‖ key prefixes, their raw CRC state from ~0, and the combine ----
-    pre = bytearray()
-    pre_off = np.zeros(n, np.uint64)
-    for r in range(n):
-        pre_off[r] = len(pre)
-        pre += struct.pack("<IIiII", int(ts[r]), int(flags[r]), int(vers[r]), int(klen[r]), int(vsz[r])) + keys[r]
-        pre += bytes((-len(pre)) % 16)
-    pre_d = torch.from_numpy(np.frombuffer(bytes(pre), np.uint8).copy()).to(dev)
-    pre_len = (20 + klen).astype(np.uint32)
-    s_hk = batch.crc32(batch.BlockBatch(pre_d, _dev_u64(pre_off, dev), _dev_u32(pre_len, dev)), final_xor=0,
-                       stream=stream)
+    # ---- header[4:24] || key prefixes (16-B aligned staging), their raw CRC state from ~0, and
+    # the combine with the value's raw CRC (datafile.go:66-76) ----
+    pre_len = (20 + klen).astype(np.int64)
+    pre_step = (pre_len + 15) // 16 * 16
+    pre_off = np.zeros(n, np.int64)
+    if n:
+        pre_off[1:] = np.cumsum(pre_step)[:-1]
+    pre = np.zeros(int(pre_step.sum()) if n else 0, np.uint8)
+    tail = np.zeros(n, dtype=[("ts", "<u4"), ("flag", "<u4"), ("ver", "<i4"), ("ksz", "<u4"), ("vsz", "<u4")])
+    tail["ts"], tail["flag"], tail["ver"], tail["ksz"], tail["vsz"] = ts, flags, vers, klen, vsz
+    if n:
+        pre[(pre_off[:, None] + np.arange(20)[None, :]).reshape(-1)] = tail.view(np.uint8).reshape(n, 20).reshape(-1)
+        kall = np.frombuffer(b"".join(keys), np.uint8)
+        if kall.size:
+            kstart = np.zeros(n, np.int64)
+            kstart[1:] = np.cumsum(klen)[:-1]
+            pre[np.repeat(pre_off + 20 - kstart, klen) + np.arange(kall.size)] = kall
+    pre_d = torch.from_numpy(pre).to(dev)
+    s_hk = batch.crc32(batch.BlockBatch(pre_d, _dev_u64(pre_off.astype(np.uint64), dev),
+                                        _dev_u32(pre_len.astype(np.uint32), dev)), final_xor=0, stream=stream)
     crc_d = torch.zeros(n, dtype=torch.int32, device=dev)
     rv = _dev_u32(raw_v, dev)
     lv = _dev_u32(vsz, dev)
     _lib.check(L.qlzx_crc32_combine(s_hk.data_ptr(), rv.data_ptr(), lv.data_ptr(), n, 0xFFFFFFFF,
                                     crc_d.data_ptr(), batch._stream(stream)), "qlzx_crc32_combine")
     crc = crc_d.cpu().numpy().view(np.uint32).copy()
-    # ---- assemble: crc ‖ header tail ‖ key ‖ value, zero padding to 256 (datafile.go:307-330) ----
+    # ---- assemble: crc || header tail || key || value, zero padding to 256 (datafile.go:307-330) ----
     rsize = (HDR + klen + vsz + 255) // 256 * 256
     roff = np.zeros(n, np.uint64)
     if n:
@@ -181,18 +213,16 @@ def encode(keys: list[bytes], values: batch.BlockBatch, flags=None, vers=None, t
     total = int(rsize.sum())
     out = torch.zeros(max(total, 1), dtype=torch.uint8, device=dev)
     # header tail + key (from the prefix staging) at off + 4
-    _copy(pre_d, pre_off, pre_len, out, roff + 4, stream)
+    _copy(pre_d, pre_off.astype(np.uint64), pre_len.astype(np.uint32), out, roff + 4, stream)
     # values: raw ones from the value buffer, compressed ones from their compress buffers
     if len(plain):
         _copy(values.data, voff[plain], vlen[plain].astype(np.uint32), out,
               roff[plain] + HDR + klen[plain].astype(np.uint64), stream)
-    by_buf = {}
-    for r, (buf, o, cl, _) in comp_body.items():
-        by_buf.setdefault(id(buf), (buf, []))[1].append((r, o, cl))
-    for buf, lst in by_buf.values():
-        rs = np.asarray([t[0] for t in lst], np.int64)
-        _copy(buf, np.asarray([t[1] for t in lst], np.uint64), np.asarray([t[2] for t in lst], np.uint32), out,
-              roff[rs] + HDR + klen[rs].astype(np.uint64), stream)
+    for b in (0, 1):
+        rs = np.nonzero(is_comp & (c_src == b))[0]
+        if len(rs):
+            _copy(bufs[b], c_off[rs], c_len[rs].astype(np.uint32), out, roff[rs] + HDR + klen[rs].astype(np.uint64),
+                  stream)
     # crc field (records are 256-B aligned, so int32 words)
     out.view(torch.int32)[torch.from_numpy((roff // 4).astype(np.int64)).to(dev)] = crc_d
     return Encoded(out[:total], roff, flags, vsz.astype(np.uint32), crc)
@@ -207,6 +237,18 @@ def _copy(src: torch.Tensor, src_off, length, dst: torch.Tensor, dst_off, stream
     so, ln, do = _dev_u64(src_off, dev), _dev_u32(length, dev), _dev_u64(dst_off, dev)
     _lib.check(L.qlzx_copy_batch(src.data_ptr(), so.data_ptr(), ln.data_ptr(), dst.data_ptr(), do.data_ptr(), n,
                                  batch._stream(stream)), "qlzx_copy_batch")
+
+
+def _gather_heads(values: batch.BlockBatch, idx: np.ndarray, k: int) -> np.ndarray:
+    """The first k bytes of each selected value (zeros past its end), uint8 [len(idx), k]."""
+    dev = values.data.device
+    sel = torch.from_numpy(idx).to(dev)
+    off = values.off[sel]
+    ln = values.length[sel].to(torch.int64)
+    ar = torch.arange(k, device=dev)
+    pos = torch.minimum(off.unsqueeze(1) + ar.unsqueeze(0), torch.tensor(values.data.numel() - 1, device=dev))
+    h = values.data[pos.reshape(-1)].reshape(len(idx), k)
+    return torch.where(ar.unsqueeze(0) < ln.unsqueeze(1), h, torch.zeros_like(h)).cpu().numpy()
 
 
 def _gather_prefix(values: batch.BlockBatch, idx: np.ndarray, k: int) -> list[bytes]:

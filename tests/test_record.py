@@ -93,3 +93,25 @@ def test_encode_policy_edges(cuda):
     assert enc.data.cpu().numpy().tobytes() == exp
     assert [int(f) for f in enc.flag] == exp_flags
     assert exp_flags[1] == 0x10000 and exp_flags[0] == exp_flags[3] == exp_flags[4] == exp_flags[5] == 0
+
+
+def test_sniff_many_matches_sniff():
+    """The vectorised policy record.encode uses (sniff_many) answers need_compress exactly,
+    per row and in row order, for crafted signatures, near misses and random heads."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    heads = [sig[1] + bytes(16) for sig in record._AV_SIGS]
+    heads += [b"MThd\x00\x00\x00\x07" + bytes(8), b"MTh", b"", b"RIFF\x01\x02\x03\x04WAVE" + bytes(4), b"ID3",
+              b"RIFF\x00\x00\x00\x00WEBPVP8 " + bytes(4), b"FORM\x01\x02\x03\x04AIFF"]
+    heads += [rng.integers(0, 256, 20, dtype=np.uint8).tobytes() for _ in range(300)]
+    H = np.zeros((len(heads), 16), np.uint8)
+    L = np.zeros(len(heads), np.int64)
+    for i, h in enumerate(heads):
+        b = np.frombuffer(h[:16], np.uint8)
+        H[i, :len(b)] = b
+        L[i] = len(h)
+    for nc in (record.NOT_COMPRESS, record.NOT_COMPRESS_SHIPPED, frozenset(),
+               frozenset({"video/avi", "audio/basic", "application/ogg", "audio/aiff"})):
+        got = record.sniff_many(H, L, nc)
+        want = np.array([record.need_compress(h, nc) for h in heads])
+        assert (got == want).all()

@@ -139,10 +139,25 @@ step_ab() {
   cat $O/ab.txt
 }
 
+# abmix TAG...: c5 (64 GiB of mixed values) and c4 (4 x 4000 MiB) per build, interleaved
+step_abmix() {
+  : > $O/abmix.txt
+  for r in $(seq ${AB_REPS:-1}); do
+    for t in "$@"; do
+      QLZX_LIB=$(lib $t) timeout -k 10 300 python3 tools/bench_c5.py --total-gib 64 --round-gib 16 > $O/c5_$t.json 2>/dev/null \
+          || { echo "c5 $t failed"; return 1; }
+      QLZX_LIB=$(lib $t) timeout -k 10 400 python3 tools/bench_replay.py --chunk-mib 4000 --files 4 --steps 2 --no-cpu \
+          --pin-records 16 > $O/c4_$t.json 2>/dev/null || { echo "c4 $t failed"; return 1; }
+      python3 -c "import json; r=json.load(open('$O/c5_$t.json')); q=json.load(open('$O/c4_$t.json')); print('$t c5', r['value'], 'c4', q['value'])" | tee -a $O/abmix.txt
+    done
+  done
+}
+
 while [ $# -gt 0 ]; do
   s=$1; shift
   case $s in
     ab) step_ab "$@" || exit 1; exit 0 ;;
+    abmix) step_abmix "$@" || exit 1; exit 0 ;;
     c2|c3|c4c5|single|rehearsal|bench) echo "== $s"; step_$s || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
