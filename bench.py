@@ -259,7 +259,7 @@ def main():
     achieved = (csum + dsum) / (kern_ms * 1e-3) / 1e9
     traffic = None
     if args.traffic_json is None and args.mode == "decompress" and kind == "text" and bs == 16384 and not args.crc:
-        args.traffic_json = os.path.join(ROOT, "profiles", "r05_c2_traffic.json")
+        args.traffic_json = os.path.join(ROOT, "profiles", "r06_c2_traffic.json")
     traffic_src = None
     if args.traffic_json and os.path.exists(args.traffic_json):
         # PMC-measured HBM bytes per block (tools/traffic.py) x blocks per launch: a committed

@@ -115,6 +115,9 @@ def lib() -> ctypes.CDLL:
     L.qlzx_last_error.restype = ctypes.c_char_p
     L.qlzx_info.argtypes = [ctypes.c_char_p, sz]
     L.qlzx_info.restype = ctypes.c_int
+    L.qlzx_read_record1.argtypes = [vp, sz, u32, u32, ctypes.c_int, vp, sz, ctypes.POINTER(sz),
+                                    ctypes.POINTER(ctypes.c_int32)]
+    L.qlzx_read_record1.restype = ctypes.c_int
     L.qlzx_service_test_fault.argtypes = [ctypes.c_int]
     L.qlzx_service_test_fault.restype = ctypes.c_int
     _lib = L

@@ -678,6 +678,39 @@ thread_local Ctx t_ctx;
 // and crc32_write's result becomes the record CRC (store/crc32.go:81-84).  The reference CPU
 // code cannot fail, so a runtime failure here (no device, a HIP error) stops the process with
 // the reason instead of returning a plausible wrong value.
+// Host CRC-32/IEEE (store/crc32.go:5-59's table, slicing-by-8) for the short slices crc32_write
+// receives; the tables are built once from the polynomial.
+#ifndef QLZX_CRC_HOST_MAX  // longest crc32_write slice folded on the host (DESIGN.md §3 "Single calls")
+#define QLZX_CRC_HOST_MAX 256
+#endif
+constexpr size_t kCrcHostMax = QLZX_CRC_HOST_MAX;
+struct HostCrcTables {
+    uint32_t t[8][256];
+    HostCrcTables() {
+        for (uint32_t b = 0; b < 256; b++) {
+            uint32_t c = b;
+            for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+            t[0][b] = c;
+        }
+        for (uint32_t b = 0; b < 256; b++)
+            for (int j = 1; j < 8; j++) t[j][b] = (t[j - 1][b] >> 8) ^ t[0][t[j - 1][b] & 0xffu];
+    }
+};
+uint32_t host_crc32(uint32_t crc, const unsigned char *p, size_t n) {
+    static const HostCrcTables T;
+    uint32_t c = crc;  // crc32_write is the raw table update (store/crc32.go:61-68): no inversions
+    for (; n >= 8; n -= 8, p += 8) {
+        uint32_t lo, hi;
+        memcpy(&lo, p, 4);
+        memcpy(&hi, p + 4, 4);
+        lo ^= c;
+        c = T.t[7][lo & 0xff] ^ T.t[6][(lo >> 8) & 0xff] ^ T.t[5][(lo >> 16) & 0xff] ^ T.t[4][lo >> 24] ^
+            T.t[3][hi & 0xff] ^ T.t[2][(hi >> 8) & 0xff] ^ T.t[1][(hi >> 16) & 0xff] ^ T.t[0][hi >> 24];
+    }
+    for (; n; n--, p++) c = T.t[0][(c ^ *p) & 0xffu] ^ (c >> 8);
+    return c;
+}
+
 [[noreturn]] void die(const char *who) {
     fprintf(stderr, "libqlzx: %s: %s (GPU runtime failure; the drop-in has no error channel)\n", who,
             t_last_error.empty() ? "unknown error" : t_last_error.c_str());
@@ -822,6 +855,66 @@ int decompress1(const char *source, void *destination, size_t *dsize_out) {
 
 extern "C" {
 
+int qlzx_read_record1(const void *value, size_t vlen, uint32_t crc_state, uint32_t crc_expect, int compressed,
+                      void *dst, size_t dst_cap, size_t *out_len, int32_t *status) {
+    if (!value && vlen) return fail(QLZX_R_BAD_ARG, "qlzx_read_record1: null value");
+    if (!out_len || !status) return fail(QLZX_R_BAD_ARG, "qlzx_read_record1: null out_len / status");
+    *out_len = 0;
+    *status = QLZX_E_RUNTIME;
+    const uint8_t *v = (const uint8_t *)value;
+    size_t dsize = 0;
+    if (compressed) {
+        if (vlen < 3 || vlen < (size_t)((v[0] & 2) ? 9 : 3)) {  // Payload.Decompress: CDecompressSafe's panic
+            // the CRC is still checked first, as readRecordAt does before the payload is used
+            const uint32_t c = vlen ? crc32_write(crc_state, (unsigned char *)value, (int)vlen) : crc_state;
+            *status = (~c != crc_expect) ? QLZX_E_CRC : QLZX_E_HEADER;
+            return QLZX_R_OK;
+        }
+        dsize = qlz_size_decompressed((const char *)value);
+        if (!dst || dst_cap < dsize) return fail(QLZX_R_BAD_ARG, "qlzx_read_record1: dst_cap below the value's dsize");
+    }
+    const bool served = vlen <= qlzx::kSvcIn - 64 &&
+                        (!compressed || (dsize <= qlzx::kSvcMaxLen && vlen <= qlzx::kSoloMaxCsize));
+    if (served) {  // one request: CRC check, then the decode, in one kernel (qlzx_service.hip)
+        Service *S = service();
+        if (!S) return QLZX_R_NO_DEVICE;
+        const uint32_t b = S->take_slot();
+        memcpy(S->in(b), value, vlen);
+        qlzx::SvcReq r{};
+        r.slot = b, r.len = (uint32_t)vlen, r.cap = (uint32_t)dsize;
+        r.arg = crc_state, r.expect = crc_expect;
+        r.mode = qlzx::kSvcVerify | (compressed ? 0u : qlzx::kSvcNoDecode);
+        const int rc = S->run(qlzx::kSvcDecode, r);
+        const qlzx::SvcDone d = *(const qlzx::SvcDone *)(S->h_done + b);
+        if (rc == QLZX_R_OK) {
+            *status = d.status;
+            if (d.status == QLZX_OK) {
+                if (compressed) memcpy(dst, S->out(b), d.out), *out_len = d.out;
+                else *out_len = vlen;
+            }
+        }
+        S->give_slot(b);
+        t_last_status = *status;
+        return rc;
+    }
+    // longer values: the general per-call paths (GPU), CRC first
+    const uint32_t c = crc32_write(crc_state, (unsigned char *)value, (int)vlen);
+    if (~c != crc_expect) {
+        *status = t_last_status = QLZX_E_CRC;
+        return QLZX_R_OK;
+    }
+    if (!compressed) {
+        *status = t_last_status = QLZX_OK;
+        *out_len = vlen;
+        return QLZX_R_OK;
+    }
+    size_t n = 0;
+    const int rc = decompress1((const char *)value, dst, &n);
+    *status = t_last_status;
+    *out_len = n;
+    return rc;
+}
+
 int qlzx_last_status(void) { return t_last_status; }
 
 int qlzx_service_test_fault(int mode) {
@@ -911,6 +1004,14 @@ size_t qlzx_go_decompress1(const char *source, size_t source_len, void *destinat
 
 uint32_t crc32_write(uint32_t crc, unsigned char *buf, int len) {
     if (len <= 0) return crc;  // store/crc32.go:65 loops zero times
+    if ((size_t)len <= kCrcHostMax) {
+        // readRecordAt / WriteRecord.getCRC pass header[4:24] and the key as slices of their own
+        // (store/datafile.go:66-76); a request round trip (~20 us) costs more than the bytes, so
+        // slices up to kCrcHostMax are folded on the calling thread.  The library still requires
+        // its device: without one the call stops the process like every drop-in.
+        if (!service()) die("crc32_write");
+        return host_crc32(crc, buf, (size_t)len);
+    }
     if ((size_t)len <= qlzx::kSvcIn - 64) {  // the request path (qlzx_service.hip)
         Service *S = service();
         if (!S) die("crc32_write");

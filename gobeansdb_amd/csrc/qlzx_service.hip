@@ -43,9 +43,13 @@ enum : uint32_t { kSvcDecode = 0, kSvcCompress = 1, kSvcCrc = 2, kSvcOps = 3 };
 
 struct SvcReq {
     uint32_t slot, len, cap, seq;
-    uint32_t arg;  // crc: initial state
-    uint32_t pad[3];
+    uint32_t arg;     // crc, and decode with kSvcVerify: the CRC state before the input bytes
+    uint32_t expect;  // decode with kSvcVerify: the stored record CRC (~state after the input)
+    uint32_t mode;    // decode: kSvcVerify and/or kSvcNoDecode (0: a plain qlz_decompress)
+    uint32_t pad;
 };
+// decode request modes (qlzx_read_record1: readRecordAt's CRC check + Payload.Decompress, one request)
+constexpr uint32_t kSvcVerify = 1, kSvcNoDecode = 2;
 struct SvcBatch {
     uint32_t n, pad[3];
     SvcReq r[kSvcBatchMax];
@@ -80,16 +84,34 @@ __global__ void __launch_bounds__(kSoloWG) k_svc_decode(SvcBatch B, const uint8_
     __shared__ __attribute__((aligned(16))) union {
         SoloLds solo;
         SmallLds small;
+        uint32_t crc[kCrcLdsWords];
     } U;
     __shared__ int32_t st;
-    __shared__ uint32_t ds;
+    __shared__ uint32_t ds, crc_s;
     const SvcReq r = B.r[blockIdx.x];
     const uint8_t *hin = h_arena + (size_t)r.slot * kSvcHostSlot;
     uint8_t *hout = (uint8_t *)hin + kSvcIn;
+    uint32_t crc = 0;
+    if (r.mode & kSvcVerify) {
+        // readRecordAt (store/datafile.go:161-168): the record CRC over the value, continued from
+        // the header[4:24] | key state, checked before anything is decoded
+        load_crc_lds(U.crc);
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const uint32_t c = wave_crc(U.crc, hin, r.len, r.arg, threadIdx.x);
+            if (threadIdx.x == 0) crc_s = c;
+        }
+        __syncthreads();
+        crc = crc_s;
+        if ((~crc != r.expect) || (r.mode & kSvcNoDecode)) {
+            svc_publish(done, r, 0, ~crc != r.expect ? QLZX_E_CRC : QLZX_OK, crc);
+            return;
+        }
+    }
     // small blocks: stream from the host slot into LDS, result straight into the host slot
     if (small_decode(U.small, hin, r.len, hout, r.cap, r.cap, &st, &ds)) {
         __syncthreads();
-        svc_publish(done, r, st == QLZX_OK ? ds : 0u, st, 0);
+        svc_publish(done, r, st == QLZX_OK ? ds : 0u, st, crc);
         return;
     }
     SoloLds &L = U.solo;
@@ -103,7 +125,7 @@ __global__ void __launch_bounds__(kSoloWG) k_svc_decode(SvcBatch B, const uint8_
     __syncthreads();
     const uint32_t n = st == QLZX_OK ? ds : 0u;
     svc_copy(hout, ddst, n, tid, kSoloWG);
-    svc_publish(done, r, n, st, 0);
+    svc_publish(done, r, n, st, crc);
 }
 
 __global__ void __launch_bounds__(256) k_svc_crc(SvcBatch B, const uint8_t *h_arena, uint8_t *d_arena, SvcDone *done) {

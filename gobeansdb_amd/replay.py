@@ -403,3 +403,34 @@ def hint_digest(offset, header, vhash, key_base: int = 0, file_id: int = 0) -> i
         m = (m * 0x01000193 ^ hdr[:, c]) & 0xFFFFFFFF
     m = (m * 0x01000193 ^ vh) & 0xFFFFFFFF
     return int(np.bitwise_xor.reduce(m))
+
+
+def read_record(rec: bytes) -> tuple[int, bytes] | None:
+    """One record as a GET reads it: readRecordAt's CRC check (store/datafile.go:161-168) and
+    Payload.Decompress (store/item.go:163-176) -- header[4:24] and the key through crc32_write
+    (the library folds such short slices on the host), then the value's CRC and its decode in ONE
+    request (qlzx_read_record1).  Returns (flag after Payload.Decompress, value), or None when the
+    record CRC does not match (readRecordAt's error).  As in the reference, a value that fails to
+    decode stays compressed with its flag unchanged."""
+    import struct
+    L = _lib.lib()
+    crc, _ts, flag, _ver, ksz, vsz = struct.unpack_from("<IIIiII", rec, 0)
+    key = rec[HDR:HDR + ksz]
+    val = bytes(rec[HDR + ksz:HDR + ksz + vsz])
+    st = L.crc32_write(0xFFFFFFFF, bytes(rec[4:HDR]), 20)
+    if ksz:
+        st = L.crc32_write(st, bytes(key), ksz)
+    comp = bool(flag & FLAG_COMPRESS)
+    cap = 0
+    if comp and len(val) >= (9 if (val and val[0] & 2) else 3):
+        cap = int.from_bytes(val[5:9], "little") if val[0] & 2 else val[2]
+    dst = ctypes.create_string_buffer(max(cap, 1))
+    out = ctypes.c_size_t(0)
+    status = ctypes.c_int32(0)
+    _lib.check(L.qlzx_read_record1(val, len(val), st, crc, int(comp), dst, cap, ctypes.byref(out),
+                                   ctypes.byref(status)), "qlzx_read_record1")
+    if status.value == _lib.E_CRC:
+        return None
+    if comp and status.value == _lib.OK:
+        return flag - FLAG_COMPRESS, dst.raw[:out.value]
+    return flag, val

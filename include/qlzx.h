@@ -247,6 +247,18 @@ int qlzx_last_status(void);
 /* Last error message of the calling thread (empty if none). */
 const char *qlzx_last_error(void);
 
+/* One record read in ONE request, as readRecordAt + Payload.Decompress use it
+ * (store/datafile.go:161-168, store/item.go:163-176): the record CRC continued from `crc_state`
+ * (crc32_write from ~0 over header[4:24] then the key) over the `vlen` value bytes is checked
+ * against the stored `crc_expect` (~state == crc_expect), and only then, when `compressed`
+ * (FLAG_COMPRESS), the value is decompressed into dst (dst_cap >= its dsize).  Replaces the
+ * value's crc32_write and the qlz_decompress of the same GET (two GPU round trips) with one.
+ * *status: QLZX_OK, QLZX_E_CRC (nothing decoded), or the decode status; *out_len: the value's
+ * length after the step (vlen when not compressed, which is not copied).  Returns a qlzx_return
+ * code (runtime failure). */
+int qlzx_read_record1(const void *value, size_t vlen, uint32_t crc_state, uint32_t crc_expect, int compressed,
+                      void *dst, size_t dst_cap, size_t *out_len, int32_t *status);
+
 /* Library/version info: fills `buf` with a short description (arch, kernels, source hash). */
 int qlzx_info(char *buf, size_t len);
 

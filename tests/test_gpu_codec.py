@@ -398,3 +398,23 @@ def test_decompress_deflated_header_csize_decodes_like_go(cuda):
         assert Decompress(small) == v
         with pytest.raises(QuicklzError):
             Decompress(c + b"\0\0\0")  # trailing bytes after the last item: C5
+
+
+def test_crc32_write_drop_in_every_length_to_600(cuda):
+    """crc32_write (store/crc32.go:61-68, a raw table update with no inversions) at every length
+    0..600 -- slices up to the library's host threshold (256 B) and the request path above it --
+    from several states, and chained over header[4:24] | key | value as readRecordAt does
+    (store/datafile.go:161-168): equal to the oracle's."""
+    from gobeansdb_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(600)
+    data = rng.integers(0, 256, 600, dtype=np.uint8).tobytes()
+    for n in range(0, 601):
+        for s0 in (0xFFFFFFFF, 0, 0x12345678):
+            assert L.crc32_write(s0, data[:n], n) == O.crc32_write(s0, data[:n]), (n, s0)
+    for klen, vlen in ((20, 4000), (250, 256), (3, 257), (100, 16384)):
+        hdr, key, val = data[:20], data[20:20 + klen], O.gen_text(5, vlen, vlen)
+        st = 0xFFFFFFFF
+        for part in (hdr, key, val):
+            st = L.crc32_write(st, part, len(part))
+        assert st ^ 0xFFFFFFFF == O.record_crc(hdr, key, val)

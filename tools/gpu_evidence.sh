@@ -42,7 +42,7 @@ step_c2() {
   kstats $O/trace $O/c2_kernel_stats.txt
   QLZX_LIB=gobeansdb_amd/libqlzx_prof.so timeout -k 10 120 python -u tools/phase_prof.py 131072 16384 2>&1 \
       | grep -v amdgpu.ids > $O/phase.txt
-  tail -3 $O/c2_kernel_stats.txt $O/phase.txt
+  tail -n 3 $O/c2_kernel_stats.txt $O/phase.txt
 }
 
 step_c3() {
@@ -56,7 +56,7 @@ step_c3() {
       python3 bench.py --config c3 --blocks 262144 --steps 2 --warmup 1 --no-cpu > $O/c3_trace.json 2> $O/c3_trace.err \
       || { tail $O/c3_trace.err; return 1; }
   kstats $O/c3trace $O/c3_kernel_stats.txt
-  cat $O/c3_traffic.json; head -5 $O/c3_kernel_stats.txt
+  cat $O/c3_traffic.json; head -n 5 $O/c3_kernel_stats.txt
 }
 
 step_c4c5() {
@@ -80,7 +80,7 @@ step_c4c5() {
   python3 tools/traffic_call.py $O/c5pmc k_order_count $RB $O/c5_traffic.json | tee $O/c5_traffic.txt || return 1
   kstats $O/c4trace $O/c4_kernels.txt
   kstats $O/c5trace $O/c5_kernels.txt
-  head -8 $O/c4_kernels.txt $O/c5_kernels.txt
+  head -n 8 $O/c4_kernels.txt $O/c5_kernels.txt
 }
 
 step_single() {
