@@ -173,6 +173,7 @@ def main():
                         "parts shorten the exposed first H2D, but each replay call reads its record counts "
                         "back to size its outputs: 512 MiB parts gave 36 GiB/s for the hints leg, 128 MiB 21, "
                         "whole 4000 MiB pieces 46)")
+    p.add_argument("--no-gc", action="store_true", help="skip the f4 GC leg (e.g. for a PMC pass over the replay)")
     p.add_argument("--pin-records", type=int, default=1024,
                    help="records per chunk compared with the oracle inside the correctness gate")
     a = p.parse_args()
@@ -367,24 +368,26 @@ def run(a, rank: int, world: int, dev):
     # recomputed CRCs (gobeansdb_amd.gc.rewrite).  Checked: every rewritten CRC equals the stored
     # one, and the rewritten chunk replays to exactly the kept records ----
     from gobeansdb_amd import gc as gcmod
+    do_gc = not getattr(a, "no_gc", False)
     c0 = chunks[0]
     ro_t = torch.from_numpy(c0["rec_off"].astype(np.int64)).to(dev)
     keep = torch.from_numpy(np.random.default_rng(a.seed).random(c0["nrec"]) < 0.7).to(dev)
-    g = gcmod.rewrite(c0["dev"], ro_t, keep)
-    torch.cuda.synchronize()
-    assert g.crc_mismatch == 0, f"gc: {g.crc_mismatch} rewritten CRCs differ"
-    nk = int(keep.sum())
-    rr = replay.replay(g.chunks[0], workspace=ws)
-    assert len(g.chunks) == 1 and rr.n == nk and not rr.end_error, (len(g.chunks), rr.n, nk)
-    kept_bytes = int(g.chunks[0].numel())
-    del rr, g
-    sync_all()
-    t = time.perf_counter()
-    for _ in range(a.steps):
+    nk, kept_bytes, gc_s = int(keep.sum()), 0, 1.0
+    if do_gc:
         g = gcmod.rewrite(c0["dev"], ro_t, keep)
-    sync_all()
-    gc_s = (time.perf_counter() - t) / a.steps
-    del g
+        torch.cuda.synchronize()
+        assert g.crc_mismatch == 0, f"gc: {g.crc_mismatch} rewritten CRCs differ"
+        rr = replay.replay(g.chunks[0], workspace=ws)
+        assert len(g.chunks) == 1 and rr.n == nk and not rr.end_error, (len(g.chunks), rr.n, nk)
+        kept_bytes = int(g.chunks[0].numel())
+        del rr, g
+        sync_all()
+        t = time.perf_counter()
+        for _ in range(a.steps):
+            g = gcmod.rewrite(c0["dev"], ro_t, keep)
+        sync_all()
+        gc_s = (time.perf_counter() - t) / a.steps
+        del g
     dev_wall, dev_ev, pipe_s, hint_s, gc_s = shard.max_over_ranks([dev_wall, dev_ev, pipe_s, hint_s, gc_s], device=dev)
     tot = shard.sum_over_ranks({"chunk": share, "out": out_mine, "records": nrec_mine, "pieces": len(pieces),
                                 "parts": len(parts), "tail_checked": tail_checked},
@@ -447,7 +450,7 @@ def run(a, rank: int, world: int, dev):
                              "note": "as buildHintFromData (store/bucket.go:89-117): the same pipeline, but the "
                                      "decompressed bodies stay on the device (they only feed Getvhash, p.Free()); "
                                      "per record offset, stored header and vhash go back (pinned D2H)"},
-        "gc": {"value": round(kept_bytes / gc_s / 2**30, 2), "unit": "GiB/s of rewritten records",
+        "gc": None if not do_gc else {"value": round(kept_bytes / gc_s / 2**30, 2), "unit": "GiB/s of rewritten records",
                "ms_per_call": round(gc_s * 1e3, 2), "records_kept": nk, "records": chunks[0]["nrec"],
                "roofline": {"bound": "hbm", "achieved": round(2 * kept_bytes / gc_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                             "unit": "GB/s", "frac": round(2 * kept_bytes / gc_s / 1e9 / HBM_PEAK_GBS, 4),

@@ -79,6 +79,23 @@ def main():
     L = _lib.lib()
     ref = O.ref()
     rows = []
+    # a 20-B crc32_write (the header slice of every record read and write)
+    h20 = [np.frombuffer(os.urandom(20), np.uint8).copy() for _ in range(a.values)]
+    for hh in h20:
+        assert L.crc32_write(0xFFFFFFFF, hh.ctypes.data, 20) == O.crc32_write(0xFFFFFFFF, hh.tobytes())
+    st_ = [0]
+
+    def c20(lib):
+        def f():
+            k = st_[0]
+            st_[0] = k + 1 if k + 1 < a.values else 0
+            lib.crc32_write(0xFFFFFFFF, h20[k].ctypes.data, 20)
+        return f
+    row20 = {"bytes": 20, "gpu_lib_crc32_us": med_us(c20(L), a.calls)}
+    if ref is not None:
+        row20["ref_crc32_us"] = med_us(c20(ref[1]), a.calls)
+    rows.append(row20)
+    print(json.dumps(row20), flush=True)
     for n in (4096, 16384, 65536):
         plains = [O.gen_text(0x5EED2026 + n, i, n) for i in range(a.values)]
         comps = [O.compress(p) for p in plains]
@@ -137,6 +154,48 @@ def main():
                                                                              scratch.ctypes.data)), a.calls)
             row["ref_decompress_cgo_us"] = med_us(cyc(cgo_decompress), a.calls)
             row["ref_crc32_us"] = med_us(cyc(lambda k: C.crc32_write(0xFFFFFFFF, src[k].ctypes.data, n)), a.calls)
+        # one GET as readRecordAt + Payload.Decompress make it (store/datafile.go:161-168,
+        # store/item.go:163-176) on a record with a compressed value: three crc32_write slices
+        # (header[4:24], key, value) then the decode; with qlzx_read_record1 the value's CRC and the
+        # decode are one request.  Correctness first, on every record.
+        from oracle import replay as R
+        recs = []
+        for k in range(nv):
+            key = b"key_%016x" % k
+            rec = R.make_record(key, comps[k], flag=R.FLAG_COMPRESS, ver=1)
+            recs.append((np.frombuffer(rec[4:24], np.uint8).copy(), np.frombuffer(key, np.uint8).copy(),
+                         int.from_bytes(rec[:4], "little")))
+        out_len = ctypes.c_size_t(0)
+        st32 = ctypes.c_int32(0)
+
+        def get_drop_ins(k, lib=L):
+            h, key, crc = recs[k]
+            s_ = lib.crc32_write(0xFFFFFFFF, h.ctypes.data, 20)
+            s_ = lib.crc32_write(s_, key.ctypes.data, len(key))
+            s_ = lib.crc32_write(s_, csrc[k].ctypes.data, len(comps[k]))
+            assert s_ ^ 0xFFFFFFFF == crc
+            return lib.qlz_decompress(csrc[k].ctypes.data, dst.ctypes.data, scratch.ctypes.data)
+
+        def get_one_request(k):
+            h, key, crc = recs[k]
+            s_ = L.crc32_write(0xFFFFFFFF, h.ctypes.data, 20)
+            s_ = L.crc32_write(s_, key.ctypes.data, len(key))
+            L.qlzx_read_record1(csrc[k].ctypes.data, len(comps[k]), s_, crc, 1, dst.ctypes.data, n,
+                                ctypes.byref(out_len), ctypes.byref(st32))
+        for k in range(nv):
+            assert get_drop_ins(k) == n and dst[:n].tobytes() == plains[k]
+            dst[:] = 0
+            get_one_request(k)
+            assert st32.value == 0 and out_len.value == n and dst[:n].tobytes() == plains[k]
+        row["gpu_get_drop_ins_us"] = med_us(cyc(get_drop_ins), a.calls)
+        row["gpu_get_read_record1_us"] = med_us(cyc(get_one_request), a.calls)
+        if ref is not None:
+            Cq = ref[1]
+
+            class _Ref:  # the reference crc32_write and qlz_decompress, called the same way
+                crc32_write = Cq.crc32_write
+                qlz_decompress = ref[0].qlz_decompress
+            row["ref_get_us"] = med_us(cyc(lambda k: get_drop_ins(k, _Ref)), a.calls)
         if a.threads:
             def mk(lib):
                 def for_thread(t):

@@ -60,7 +60,7 @@ step_c3() {
 }
 
 step_c4c5() {
-  local C4="tools/bench_replay.py --chunk-mib 1000 --files 2 --steps 2 --no-cpu --pin-records 64"
+  local C4="tools/bench_replay.py --chunk-mib 1000 --files 2 --steps 2 --no-cpu --pin-records 64 --no-gc"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c4trace -o trace -- python3 $C4 \
       > $O/c4_trace.json 2> $O/c4_trace.err || { tail $O/c4_trace.err; return 1; }
   for c in FETCH_SIZE WRITE_SIZE; do
