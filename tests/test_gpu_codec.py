@@ -220,6 +220,41 @@ def test_record_fused_crc_verify(cuda, golden, general):
             assert s == 0 and o == v
 
 
+# max_dsize 16384 and 65536: the two chunk regimes of the batch decoder (uniform / mixed sizes),
+# both with the record-CRC prologue of k_dec_chunk4<true>.
+@pytest.mark.parametrize("max_dsize", [16384, 65536])
+def test_batch_crc_verify_every_length(cuda, max_dsize):
+    """store/datafile.go:161-168 through qlzx_decompress_batch: the CRC continued from a per-block
+    state over blocks of every length 0..699 and 300 longer ones (to 17,000 B), packed at unaligned
+    offsets; every 7th stored CRC is wrong and must give QLZX_E_CRC, the others must not."""
+    import torch
+    from gobeansdb_amd import _lib, batch
+    rng = np.random.default_rng(5)
+    lens = list(range(700)) + [int(x) for x in rng.integers(700, 17000, 300)]
+    blocks = []
+    for n in lens:
+        b = bytearray(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        if n >= 3:  # a short level-3 stored header with dsize 16: no block goes to the general path
+            b[0], b[1], b[2] = 0x0C, n & 0xFF, 16
+        blocks.append(bytes(b))
+    states = rng.integers(0, 2 ** 32, len(lens), dtype=np.uint64).astype(np.uint32)
+    want = np.array([O.crc32_write(int(s), b) ^ 0xFFFFFFFF for s, b in zip(states, blocks)], np.uint32)
+    bad = np.arange(len(lens)) % 7 == 3
+    expect = want ^ np.where(bad, np.uint32(0x1000), np.uint32(0))
+    src = batch.BlockBatch.from_bytes(blocks)
+    out = batch.BlockBatch.empty_for([256] * len(lens))
+    cap_t = torch.full((len(lens),), 256, dtype=torch.int32, device="cuda")
+    s_t = torch.tensor(states.view(np.int32), device="cuda")
+    e_t = torch.tensor(expect.view(np.int32), device="cuda")
+    _, st, crc = batch.decompress(src, out, dst_cap=cap_t, crc_state=s_t, crc_expect=e_t, max_dsize=max_dsize)
+    torch.cuda.synchronize()
+    crc = crc.cpu().numpy().view(np.uint32)
+    st = st.cpu().numpy()
+    assert (crc == want).all(), np.nonzero(crc != want)[0][:10]
+    assert (st[bad] == _lib.E_CRC).all()
+    assert (st[~bad] != _lib.E_CRC).all()
+
+
 @pytest.mark.parametrize("crc", [False, True])
 def test_multi_chunk_overlap_round_trip(cuda, crc):
     """More blocks than one decode chunk (262144 when max_dsize <= 16 KiB, chunk_blocks in

@@ -139,6 +139,18 @@ step_ab() {
   cat $O/ab.txt
 }
 
+# sqab TAG...: one SQ pass (LDS and issue counters) of a 131,072-block c2 call per build (K1/K2 lines)
+step_sqab() {
+  : > $O/sqab.txt
+  for t in "$@"; do
+    QLZX_LIB=$(lib $t) timeout -s KILL 90 rocprofv3 --pmc ${SQ_COUNTERS:-SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES} \
+        --output-format csv -d $O/sqab/$t -o sq -- python3 tools/exp_time.py 131072 16384 1 > $O/sqab_$t.txt 2>&1 \
+        || { echo "sqab $t failed"; tail -3 $O/sqab_$t.txt; return 1; }
+    { echo "== $t"; python3 tools/pmc_sum.py $O/sqab/$t | grep -A9 "k_dec_"; } >> $O/sqab.txt || return 1
+  done
+  cat $O/sqab.txt
+}
+
 # abmix TAG...: c5 (64 GiB of mixed values) and c4 (4 x 4000 MiB) per build, interleaved
 step_abmix() {
   : > $O/abmix.txt
@@ -158,6 +170,7 @@ while [ $# -gt 0 ]; do
   case $s in
     ab) step_ab "$@" || exit 1; exit 0 ;;
     abmix) step_abmix "$@" || exit 1; exit 0 ;;
+    sqab) step_sqab "$@" || exit 1; exit 0 ;;
     c2|c3|c4c5|single|rehearsal|bench) echo "== $s"; step_$s || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
