@@ -925,7 +925,11 @@ int qlzx_service_test_fault(int mode) {
         return e && e[0] == '1';
     }();
     if (!armed) return fail(QLZX_R_BAD_ARG, "qlzx_service_test_fault: test hooks are off (QLZX_TEST_HOOKS=1)");
-    if (mode != 1 && mode != 2) return fail(QLZX_R_BAD_ARG, "qlzx_service_test_fault: mode is 1 or 2");
+    if (mode < 1 || mode > 4) return fail(QLZX_R_BAD_ARG, "qlzx_service_test_fault: mode is 1 to 4");
+    if (mode >= 3) {  // the batch decoder's next K1 (3) or K2 (4) launch
+        qlzx::g_batch_fault.store(mode, std::memory_order_release);
+        return QLZX_R_OK;
+    }
     Service *S = service();
     if (!S) return QLZX_R_NO_DEVICE;
     S->fault.store(mode, std::memory_order_release);

@@ -282,6 +282,15 @@ int launch_k2_nocrc(uint32_t grid, hipStream_t s, const qlzx_blocks &b, uint32_t
                     uint32_t first, uint32_t cnt, const BlkInfo *info, const GroupRec *recs, uint32_t gmax,
                     const uint32_t *order, bool big);
 #endif
+// Test hook (qlzx_service_test_fault modes 3 / 4, inert unless QLZX_TEST_HOOKS=1): the next K1 /
+// K2 launch of a batch call is replaced by a launch failure, so the caller's error path runs.
+inline std::atomic<int> g_batch_fault{0};
+inline int batch_fault(int kernel) {
+    int k = kernel;
+    return g_batch_fault.load(std::memory_order_relaxed) == kernel && g_batch_fault.compare_exchange_strong(k, 0)
+               ? (int)hipErrorLaunchFailure
+               : 0;
+}
 // K1's grid: one wave per 64 blocks (persistent K1 waves, 512-2048 of them, made K1 the critical
 // path: c2 24.2-35.7 ms against 23.8, DESIGN.md history, round 6)
 inline uint32_t k1_grid(uint32_t cnt) { return (cnt + kParseWG - 1) / kParseWG; }
@@ -388,6 +397,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         // QLZX_K1_KMAX_MIX (10) for mixed sizes (c4: 377 vs 363 GiB/s; c5 580 vs 560)
 #if QLZX_SPLIT_K1
         // the helpers return hipGetLastError(), which also clears the error: keep it here
+        if (const int ef = batch_fault(3)) return ef;
         if (const int e1 = launch_k1_parse6(k1_grid(cnt), s1, b, dst_cap, dsize, status, first, cnt, info, recs,
                                gmax, order, max_dsize, max_dsize > 16384 ? (uint32_t)QLZX_K1_KMAX_MIX : (uint32_t)QLZX_K1_KMAX_UNI))
             return e1;
@@ -397,6 +407,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
 #endif
         if (overlap) (void)hipEventRecord(ev_k1[c & 1], s1), (void)hipStreamWaitEvent(s, ev_k1[c & 1], 0);
         // one kernel for every block size: the LDS window slides over longer blocks
+        if (const int ef = batch_fault(4)) return ef;
         if (crc)
             hipLaunchKernelGGL(k_dec_chunk4<true>, dim3(cnt), dim3(64), 0, s, b, dsize, status, first, cnt, info,
                                recs, gmax, (const uint32_t *)order, crc_state, crc_expect, crc_out);

@@ -268,7 +268,8 @@ int qlzx_info(char *buf, size_t len);
  * current device's service launches fails -- mode 1: its kernel runs but publishes no
  * completion (caught through the batch event), mode 2: the launch itself fails.  Every request
  * of that batch then fails with QLZX_R_HIP (qlzx_compress1 returns 0, the quicklz.h drop-ins
- * stop the process).  Returns a qlzx_return code. */
+ * stop the process).  For qlzx_decompress_batch: mode 3 / 4 makes its next K1 / K2 launch fail,
+ * and the call returns QLZX_R_HIP.  Returns a qlzx_return code. */
 int qlzx_service_test_fault(int mode);
 
 #ifdef __cplusplus

@@ -100,4 +100,29 @@ def test_service_batch_failure_is_reported(cuda, mode, msg):
     for _ in range(3 * 64):  # more than the slot and event pools: nothing leaked
         n = L.qlzx_compress1(v, dst, len(v), 0)
         assert dst.raw[:n] == O.compress(v)
-    assert L.qlzx_service_test_fault(3) != 0
+    assert L.qlzx_service_test_fault(5) != 0
+
+
+@pytest.mark.parametrize("mode", [3, 4])
+def test_batch_launch_failure_is_returned(cuda, mode):
+    """qlzx_decompress_batch returns QLZX_R_HIP when its K1 (mode 3) or K2 (mode 4) launch fails
+    (the split build's launch helpers report through their return value), and the next call on
+    the same workspace decodes normally."""
+    import torch
+    from gobeansdb_amd import _lib, batch
+    L = _lib.lib()
+    lens = [16384] * 3000
+    plain = batch.synth("text", 11, lens)
+    comp, cs, st, _ = batch.compress(plain, max_len=16384)
+    torch.cuda.synchronize()
+    src = batch.BlockBatch(comp.data, comp.off, cs)
+    out = batch.BlockBatch.empty_for(lens)
+    ws = batch.Workspace(torch.device("cuda"))
+    assert L.qlzx_service_test_fault(mode) == 0
+    with pytest.raises(_lib.QlzxError, match="decode_wave launch"):
+        batch.decompress(src, out, max_dsize=16384, workspace=ws)
+    torch.cuda.synchronize()
+    dsz, st, _ = batch.decompress(src, out, max_dsize=16384, workspace=ws)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    assert torch.equal(out.data, plain.data)
