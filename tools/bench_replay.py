@@ -182,7 +182,7 @@ def main():
 
 
 HBM_PEAK_GBS = 8000.0
-C4_TRAFFIC = os.path.join(ROOT, "profiles", "r05_c4_traffic.json")
+C4_TRAFFIC = os.path.join(ROOT, "profiles", "r06_c4_traffic.json")
 
 
 def committed_traffic(step_chunk_bytes: float, path: str = C4_TRAFFIC) -> dict:
