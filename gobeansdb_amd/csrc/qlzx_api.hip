@@ -111,9 +111,10 @@ int qlz_get_setting(int setting) {  // quicklz.c:31-58 as built by quicklz.h:25-
 /* ---------------- batch device API ---------------- */
 
 size_t qlzx_decompress_workspace_size(uint32_t n, uint32_t max_dsize) {
-    // two halves for batches of more than one chunk: K1/K2 of consecutive chunks overlap
+    // two halves for batches of more than one chunk: K1/K2 of consecutive chunks overlap (three
+    // for mixed sizes over three chunks or more: the last chunk's K1 starts first)
     const size_t one = qlzx::decode_wave_ws_bytes(n, max_dsize);
-    size_t ws = n > qlzx::first_chunk_blocks(max_dsize) ? 2 * one : one;
+    size_t ws = qlzx::decode_wave_halves(n, max_dsize) * one;
     if (max_dsize > QLZX_FAST_MAX_DSIZE)  // large values: the pending list and the whole-GPU decoder
         ws += align_up((size_t)n * sizeof(qlzx::HugeItem) + 256, 256) + qlzx::huge_ws_layout(max_dsize, nullptr, nullptr);
     return ws;

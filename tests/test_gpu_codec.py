@@ -255,16 +255,22 @@ def test_batch_crc_verify_every_length(cuda, max_dsize):
     assert (st[~bad] != _lib.E_CRC).all()
 
 
-@pytest.mark.parametrize("crc", [False, True])
-def test_multi_chunk_overlap_round_trip(cuda, crc):
-    """More blocks than one decode chunk (262144 when max_dsize <= 16 KiB, chunk_blocks in
-    qlzx_decode_wave.hip): K1 of chunk c+1 runs on the side stream while K2 of chunk c runs (two
-    workspace halves).  Every block must round-trip, and with crc the fused record CRC must equal
-    a separate CRC pass over the compressed values."""
+# (crc, max_dsize): the uniform regime (chunks of 262144 blocks, two workspace halves) and the
+# mixed one (max_dsize > 16 KiB: chunks of 131072; at three chunks the last chunk's K1 starts
+# first in a third workspace region)
+@pytest.mark.parametrize("crc,mixed", [(False, False), (True, False), (False, True), (True, True)])
+def test_multi_chunk_overlap_round_trip(cuda, crc, mixed):
+    """More blocks than one decode chunk (chunk_blocks in qlzx_decode_wave.hip): K1 of chunk c+1
+    runs on the side stream while K2 of chunk c runs.  Every block must round-trip, and with crc
+    the fused record CRC must equal a separate CRC pass over the compressed values."""
     import torch
-    from gobeansdb_amd import batch
+    from gobeansdb_amd import _lib, batch
     n = 262144 + 9000
     lens = [256 + (i * 37) % 1800 for i in range(n)]
+    max_dsize = 32768 if mixed else max(lens)
+    if mixed:  # three chunks, so the third workspace region is asked for
+        L = _lib.lib()
+        assert L.qlzx_decompress_workspace_size(n, max_dsize) > 2.5 * L.qlzx_decompress_workspace_size(131072, max_dsize)
     plain = batch.synth("text", 77, lens)
     comp, cs, st, _ = batch.compress(plain, max_len=max(lens))
     assert int((st != 0).sum()) == 0
@@ -273,7 +279,7 @@ def test_multi_chunk_overlap_round_trip(cuda, crc):
     kw = {}
     if crc:
         kw = dict(crc_state=torch.full((n,), -1, dtype=torch.int32, device="cuda"), want_crc=True)
-    dsz, st2, crc_out = batch.decompress(src, out, max_dsize=max(lens), **kw)
+    dsz, st2, crc_out = batch.decompress(src, out, max_dsize=max_dsize, **kw)
     torch.cuda.synchronize()
     assert int((st2 != 0).sum()) == 0
     assert torch.equal(dsz, plain.length)
