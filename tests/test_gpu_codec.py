@@ -270,7 +270,7 @@ def test_multi_chunk_overlap_round_trip(cuda, crc, mixed):
     max_dsize = 32768 if mixed else max(lens)
     if mixed:  # three chunks, so the third workspace region is asked for
         L = _lib.lib()
-        assert L.qlzx_decompress_workspace_size(n, max_dsize) > 2.5 * L.qlzx_decompress_workspace_size(131072, max_dsize)
+        assert L.qlzx_decompress_workspace_size(n, max_dsize) > 3.2 * L.qlzx_decompress_workspace_size(100000, max_dsize)
     plain = batch.synth("text", 77, lens)
     comp, cs, st, _ = batch.compress(plain, max_len=max(lens))
     assert int((st != 0).sum()) == 0
