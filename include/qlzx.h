@@ -112,7 +112,11 @@ typedef struct qlzx_blocks {
  * whole-GPU decoder's scratch: about 31.7 x max_dsize bytes (8 u16 jump levels over 1.5 x
  * max_dsize plus a u32 source index per output byte), e.g. 1.66 GB at the 50 MiB body limit.
  * qlzx_decompress_workspace_size includes it; size max_dsize from the largest header dsize
- * actually pending (as replay does), not from a configured bound. */
+ * actually pending (as replay does), not from a configured bound.
+ * Workspace of the batch decoder itself: one region per chunk in flight -- 1 for a call of one
+ * chunk, 2 when K1 of the next chunk overlaps K2 of this one, 3 for calls of values over 16 KiB
+ * in three chunks or more (the last chunk's K1 starts first).  A smaller workspace (at least one
+ * region) still decodes, with less overlap. */
 size_t qlzx_decompress_workspace_size(uint32_t n, uint32_t max_dsize);
 int qlzx_decompress_batch(const qlzx_blocks *b, const uint32_t *dst_cap, uint32_t *dsize,
                           int32_t *status, const uint32_t *crc_state, const uint32_t *crc_expect,
