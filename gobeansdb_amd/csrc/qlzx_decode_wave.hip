@@ -72,20 +72,27 @@ inline size_t decode_wave_ws_bytes(uint32_t n, uint32_t max_dsize) {
            1024 + 256;                                                            // order aux
 }
 
-// Workspace halves of a call (qlzx_decompress_workspace_size): 1 for a single chunk, 2 so K1 of
-// chunk c+1 runs beside K2 of chunk c, 3 for calls of mixed sizes over at least three chunks: the
-// last chunk (the longest values, whose one-lane-per-block K1 is the longest) gets a region of
-// its own and its K1 starts with the first one (QLZX_LAST_K1_EARLY).
+// Workspace regions of a call (qlzx_decompress_workspace_size): 1 for a single chunk, 2 so K1 of
+// chunk c+1 runs beside K2 of chunk c, and for calls of mixed sizes over three chunks or more one
+// more region for each of the last QLZX_LAST_K1_EARLY chunks (the longest values, whose
+// one-lane-per-block K1s are the longest): their K1s start with the first one.  One early chunk:
+// c5 rounds of 15.4 GiB 616.8 GiB/s (two runs) against 610.0 with two and 606.3 with none; two
+// early K1s hold enough LDS (8 KiB per K1 wave) to slow the first K2s 4x (profiles/r06_mixed_ab.txt).
 #ifndef QLZX_LAST_K1_EARLY
 #define QLZX_LAST_K1_EARLY 1
 #endif
+inline uint32_t decode_wave_early(uint32_t nchunks, uint32_t max_dsize) {
+    if (max_dsize <= 16384 || nchunks < 3) return 0u;
+    const uint32_t e = nchunks - 2;  // two regions stay for the chunks before
+    return e < (uint32_t)QLZX_LAST_K1_EARLY ? e : (uint32_t)QLZX_LAST_K1_EARLY;
+}
 inline uint32_t decode_wave_chunks(uint32_t n, uint32_t max_dsize) {
     const uint32_t c0 = first_chunk_blocks(max_dsize), cb = chunk_blocks(max_dsize);
     return n <= c0 ? 1u : 1u + (n - c0 + cb - 1) / cb;
 }
 inline uint32_t decode_wave_halves(uint32_t n, uint32_t max_dsize) {
     const uint32_t nc = decode_wave_chunks(n, max_dsize);
-    return nc == 1 ? 1u : (QLZX_LAST_K1_EARLY && max_dsize > 16384 && nc >= 3 ? 3u : 2u);
+    return nc == 1 ? 1u : 2u + decode_wave_early(nc, max_dsize);
 }
 
 // ---------------------------------------------------------- block order ----
@@ -332,8 +339,8 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     // per host thread (the batch API is re-entrant like the reference) and per device: the
     // side stream and events are created on the device that owns `s`
     struct Side {  // destroyed with the thread (Go runs cgo calls on many OS threads)
-        hipStream_t st = nullptr, st2 = nullptr;
-        hipEvent_t k1[2] = {}, k2[2] = {}, order = nullptr, last = nullptr;
+        hipStream_t st = nullptr, st2 = nullptr, st3 = nullptr;
+        hipEvent_t k1[2] = {}, k2[2] = {}, order = nullptr, last[2] = {};
         ~Side() {
             if (!st || g_hip_down.load()) return;
             for (int j = 0; j < 2; j++) {
@@ -341,14 +348,16 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
                 if (k2[j]) (void)hipEventDestroy(k2[j]);
             }
             if (order) (void)hipEventDestroy(order);
-            if (last) (void)hipEventDestroy(last);
+            for (int j = 0; j < 2; j++)
+                if (last[j]) (void)hipEventDestroy(last[j]);
+            if (st3) (void)hipStreamDestroy(st3);
             if (st2) (void)hipStreamDestroy(st2);
             (void)hipStreamDestroy(st);
         }
     };
     thread_local Side sides[kMaxDevices];
-    hipStream_t side = nullptr, side2 = nullptr;
-    hipEvent_t *ev_k1 = nullptr, *ev_k2 = nullptr, ev_order = nullptr, ev_last = nullptr;
+    hipStream_t side = nullptr, side2 = nullptr, side3 = nullptr;
+    hipEvent_t *ev_k1 = nullptr, *ev_k2 = nullptr, ev_order = nullptr, *ev_last = nullptr;
     if (overlap) {
         int dev = 0, cur = 0;
         if (s) {
@@ -366,8 +375,9 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
             if (cur != dev) (void)hipSetDevice(dev);
             hipError_t e = hipStreamCreateWithFlags(&sd.st, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&sd.st2, hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&sd.st3, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&sd.order, hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&sd.last, hipEventDisableTiming);
+            for (int j = 0; j < 2 && e == hipSuccess; j++) e = hipEventCreateWithFlags(&sd.last[j], hipEventDisableTiming);
             for (int j = 0; j < 2 && e == hipSuccess; j++) {
                 e = hipEventCreateWithFlags(&sd.k1[j], hipEventDisableTiming);
                 if (e == hipSuccess) e = hipEventCreateWithFlags(&sd.k2[j], hipEventDisableTiming);
@@ -377,6 +387,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         }
         side = sd.st;
         side2 = sd.st2;
+        side3 = sd.st3;
         ev_k1 = sd.k1;
         ev_k2 = sd.k2;
         ev_order = sd.order;
@@ -390,16 +401,18 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
     // rounds: 560 vs 620 GiB/s) and uniform 16 KiB chunks keep one side stream: there concurrent
     // K1s only compete with the K2s.
     const bool split_k1 = overlap && max_dsize > 16384 && b.n <= chunk0 + chunk;  // two chunks (c4's calls)
-    // Calls of mixed sizes over three chunks or more (c5's rounds): the last chunk holds the
-    // longest values, and its K1 (longest per lane, at low occupancy) ran after K2 of the chunk
-    // before last had freed a workspace half, in front of the last K2 (c5: 7.5 of an 18.7 ms
-    // call).  With a third workspace region it starts on the second side stream right after the
-    // block order, beside everything else.
+    // Calls of mixed sizes over three chunks or more (c5's rounds): the last chunks hold the
+    // longest values, and their K1s (longest per lane, at low occupancy) ran after K2 of the chunk
+    // two before had freed a workspace half, in front of their K2s (c5: the last K1 took 7.5 of
+    // an 18.7 ms call).  With a region of their own, the K1s of the last `early` chunks start on
+    // side streams 2 and 3 right after the block order, beside everything else.
     const uint32_t nchunks = decode_wave_chunks(b.n, max_dsize);
-    const bool early_last = overlap && decode_wave_halves(b.n, max_dsize) == 3 && ws_bytes >= 3 * one;
-    const uint32_t first_last = chunk0 + (nchunks - 2) * chunk;
+    uint32_t early = overlap ? decode_wave_early(nchunks, max_dsize) : 0u;
+    while (early && ws_bytes < (2 + early) * one) early--;  // as many regions as the caller gave
+    const uint32_t c_early = nchunks - early;                // first chunk whose K1 starts early
     if (overlap) (void)hipEventRecord(ev_k2[1], s), (void)hipStreamWaitEvent(side, ev_k2[1], 0);
-    if (split_k1 || early_last) (void)hipStreamWaitEvent(side2, ev_k2[1], 0);
+    if (split_k1 || early) (void)hipStreamWaitEvent(side2, ev_k2[1], 0);
+    if (early > 1) (void)hipStreamWaitEvent(side3, ev_k2[1], 0);
     if (sort) {  // block order of the whole call, ahead of the first K1 (workspace half 0)
         hipStream_t s1 = overlap ? side : s;
         uint32_t *aux = (uint32_t *)((uint8_t *)ws + o_aux);
@@ -408,37 +421,43 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
         hipLaunchKernelGGL(k_order_count, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, aux);
         hipLaunchKernelGGL(k_order_scatter, g, dim3(kOrderWG), 0, s1, b.src_len, b.n, aux,
                            (uint32_t *)((uint8_t *)ws + o_list));
-        if (split_k1 || early_last) (void)hipEventRecord(ev_order, side), (void)hipStreamWaitEvent(side2, ev_order, 0);
+        if (split_k1 || early) {
+            (void)hipEventRecord(ev_order, side), (void)hipStreamWaitEvent(side2, ev_order, 0);
+            if (early > 1) (void)hipStreamWaitEvent(side3, ev_order, 0);
+        }
     }
-    if (early_last) {
-        uint8_t *w = (uint8_t *)ws + 2 * one;
-        const uint32_t cnt = b.n - first_last;
-        uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first_last : nullptr;
+    for (uint32_t j = 0; j < early; j++) {  // the longest chunk first
+        const uint32_t ce = nchunks - 1 - j;
+        const uint32_t fe = chunk0 + (ce - 1) * chunk;
+        const uint32_t cnt = (ce == nchunks - 1 ? b.n : fe + chunk) - fe;
+        uint8_t *w = (uint8_t *)ws + (2 + (ce - c_early)) * one;
+        uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + fe : nullptr;
+        hipStream_t se = j == 0 ? side2 : side3;
         if (const int ef = batch_fault(3)) return ef;
 #if QLZX_SPLIT_K1
-        if (const int e1 = launch_k1_parse6(k1_grid(cnt), side2, b, dst_cap, dsize, status, first_last, cnt,
-                                            (BlkInfo *)w, (GroupRec *)(w + o_rec), gmax, order, max_dsize,
+        if (const int e1 = launch_k1_parse6(k1_grid(cnt), se, b, dst_cap, dsize, status, fe, cnt, (BlkInfo *)w,
+                                            (GroupRec *)(w + o_rec), gmax, order, max_dsize,
                                             (uint32_t)QLZX_K1_KMAX_MIX))
             return e1;
 #else
-        hipLaunchKernelGGL(k_dec_parse6, dim3(k1_grid(cnt)), dim3(kParseWG), 0, side2, b, dst_cap, dsize, status,
-                           first_last, cnt, (BlkInfo *)w, (GroupRec *)(w + o_rec), gmax, order, max_dsize,
+        hipLaunchKernelGGL(k_dec_parse6, dim3(k1_grid(cnt)), dim3(kParseWG), 0, se, b, dst_cap, dsize, status, fe,
+                           cnt, (BlkInfo *)w, (GroupRec *)(w + o_rec), gmax, order, max_dsize,
                            (uint32_t)QLZX_K1_KMAX_MIX);
 #endif
-        (void)hipEventRecord(ev_last, side2);
+        (void)hipEventRecord(ev_last[ce - c_early], se);
     }
     uint32_t c = 0;
     for (uint32_t first = 0, cnt = 0; first < b.n; first += cnt, c++) {
         const uint32_t cap = c == 0 ? chunk0 : chunk;
         cnt = b.n - first < cap ? b.n - first : cap;
-        const bool last_early = early_last && c == nchunks - 1;  // its K1 is already queued on side2
-        uint8_t *w = (uint8_t *)ws + (last_early ? 2 * one : overlap ? (c & 1) * one : 0);
+        const bool last_early = c >= c_early;  // its K1 is already queued on side stream 2 or 3
+        uint8_t *w = (uint8_t *)ws + (last_early ? (2 + (c - c_early)) * one : overlap ? (c & 1) * one : 0);
         BlkInfo *info = (BlkInfo *)w;
         GroupRec *recs = (GroupRec *)(w + o_rec);
         uint32_t *order = sort ? (uint32_t *)((uint8_t *)ws + o_list) + first : nullptr;
         hipStream_t s1 = overlap ? (split_k1 && (c & 1) ? side2 : side) : s;
         if (last_early) {
-            (void)hipStreamWaitEvent(s, ev_last, 0);
+            (void)hipStreamWaitEvent(s, ev_last[c - c_early], 0);
         } else {
             if (overlap && c >= 2) (void)hipStreamWaitEvent(s1, ev_k2[c & 1], 0);  // K2(c-2) freed this half
             // K1's step budget per iteration: QLZX_K1_KMAX_UNI (12) for uniform 16 KiB calls,
