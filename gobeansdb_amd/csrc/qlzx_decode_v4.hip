@@ -128,10 +128,11 @@ __device__ __forceinline__ void k1_parse_wave(uint8_t *ring, uint32_t lane, uint
     // time (+32 per step: +0.42 ms), DESIGN.md §3.
     const uint32_t lane16 = lane << 4;
     auto rd32 = [&](uint32_t x) __attribute__((always_inline)) -> uint32_t {  // ring_rd32<S>(ring, x, lane)
-        static_assert(S * kPieces == 8, "ring address below assumes 8 pieces of 1 KiB");
+        constexpr uint32_t PB = S * kPieces == 8 ? 3u : S * kPieces == 4 ? 2u : 4u;  // log2(pieces of 1 KiB)
+        static_assert((1u << PB) == S * kPieces, "ring address below assumes 4, 8 or 16 pieces of 1 KiB");
         const uint32_t x4 = x + 4;
-        const uint32_t a1 = (__builtin_amdgcn_ubfe(x, 4, 3) << 10) | ((x & 12u) | lane16);
-        const uint32_t a2 = (__builtin_amdgcn_ubfe(x4, 4, 3) << 10) | ((x4 & 12u) | lane16);
+        const uint32_t a1 = (__builtin_amdgcn_ubfe(x, 4, PB) << 10) | ((x & 12u) | lane16);
+        const uint32_t a2 = (__builtin_amdgcn_ubfe(x4, 4, PB) << 10) | ((x4 & 12u) | lane16);
         const uint32_t lo = *(const uint32_t *)(ring + a1);
         const uint32_t hi = *(const uint32_t *)(ring + a2);
         return __builtin_amdgcn_alignbyte(hi, lo, x);

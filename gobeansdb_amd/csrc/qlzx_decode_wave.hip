@@ -55,7 +55,10 @@ constexpr uint32_t kPieces = kRoundBytes / 16;
 // K1's LDS ring: kRingSlots rounds of kRoundBytes per lane (8 KiB per wave).  An 8-round ring
 // for chunks of few waves gained 0.16 ms on c4's 4.4 ms chunk of long streams (their lanes are
 // bound by the serial step chain, not by the load latency) and was dropped in round 5.
-constexpr uint32_t kRingSlots = 4;
+#ifndef QLZX_K1_SLOTS
+#define QLZX_K1_SLOTS 4
+#endif
+constexpr uint32_t kRingSlots = QLZX_K1_SLOTS;
 template <uint32_t S>
 constexpr uint32_t kRingWaveS = S * kRoundBytes * 64;
 __host__ __device__ inline uint32_t groups_max(uint32_t max_dsize) { return max_dsize / 31u + 2u; }
