@@ -10,7 +10,7 @@
 //
 // K2 k_dec_chunk4  one WAVE per block, 64 items per batch and 256 output bytes per chunk:
 //     * ITEM PHASE: token position from the GroupRec, branch-free token decode, DPP scan of the
-//       output lengths; item i leaves ONE u32 key (d << 16 | off) in a 512-entry marker ring
+//       output lengths; item i leaves ONE u32 key (d << 16 | off) in a 256-entry marker ring
 //       at slot d (off = 0 for a literal, whose byte also goes to the output window);
 //     * CHUNK PHASE: lane l owns bytes c + 4l .. c + 4l + 3.  The keys grow with d, so the
 //       forward fill of "the item covering byte p" is a max-scan (in-lane max + DPP max across
