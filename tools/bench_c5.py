@@ -71,12 +71,12 @@ def c5_traffic(round_out_bytes: int) -> dict:
     """PMC HBM bytes of one round (one batch decompress of the resident set): the committed
     per-output-byte figure (tools/traffic_call.py over a rocprofv3 FETCH_SIZE / WRITE_SIZE run)
     x this round's decompressed bytes; null when the profile is absent."""
-    path = os.path.join(ROOT, "profiles", "r05_c5_traffic.json")
+    path = os.path.join(ROOT, "profiles", "r06_c5_traffic.json")
     if not os.path.exists(path):
         return {"traffic": None}
     tj = json.load(open(path))
     return {"traffic": round(tj["hbm_bytes_per_call_byte"] * round_out_bytes),
-            "traffic_source": f"profiles/r05_c5_traffic.json: {tj['hbm_bytes_per_call_byte']:.3f} HBM B per output "
+            "traffic_source": f"profiles/r06_c5_traffic.json: {tj['hbm_bytes_per_call_byte']:.3f} HBM B per output "
                               f"byte (PMC, one round of {tj['call_bytes'] / 2**30:.1f} GiB out) x bytes per round"}
 
 
