@@ -376,7 +376,7 @@ inline int launch_decode_wave(const qlzx_blocks &b, const uint32_t *dst_cap, uin
             note_hip_up();
             (void)hipGetDevice(&cur);
             if (cur != dev) (void)hipSetDevice(dev);
-hipError_t e = hipStreamCreateWithFlags(&sd.st, hipStreamNonBlocking);
+            hipError_t e = hipStreamCreateWithFlags(&sd.st, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&sd.st2, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&sd.st3, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&sd.order, hipEventDisableTiming);
